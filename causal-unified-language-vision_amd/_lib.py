@@ -1,0 +1,98 @@
+"""ctypes binding of libcullavo_hip.so.
+
+The argument types are generated from ``include/cullavo_capi.h`` itself, so the Python side
+cannot drift from the C-ABI: every ``int cullavo_*(...)`` / ``size_t cullavo_*(...)``
+declaration in the header becomes a bound function with matching ctypes argtypes.
+There is no CPU fallback: a missing or unloadable library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcullavo_hip.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "cullavo_capi.h")
+
+_CTYPE = {
+    "int": ctypes.c_int,
+    "int64_t": ctypes.c_int64,
+    "float": ctypes.c_float,
+    "size_t": ctypes.c_size_t,
+}
+
+DT_F32 = 0
+DT_BF16 = 1
+ACT_NONE = 0
+ACT_GELU = 1
+ACT_QUICK_GELU = 2
+
+_lib = None
+_decls: dict[str, tuple[str, list[tuple[str, str]]]] | None = None
+
+
+def parse_header(path: str = HEADER) -> dict[str, tuple[str, list[tuple[str, str]]]]:
+    """Return {name: (return type, [(c type, arg name), ...])} for every cullavo_* function."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", " ", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"(int|size_t|const char\s*\*)\s+(cullavo_\w+)\s*\(([^)]*)\)\s*;", txt):
+        ret, name, args = m.group(1), m.group(2), m.group(3).strip()
+        params = []
+        if args and args != "void":
+            for a in args.split(","):
+                a = " ".join(a.split())
+                am = re.match(r"(.*?)(\w+)$", a)
+                ctype, pname = am.group(1).strip(), am.group(2)
+                params.append((ctype, pname))
+        out[name] = (" ".join(ret.split()), params)
+    return out
+
+
+def _argtype(ctype: str):
+    if "*" in ctype:
+        return ctypes.c_void_p
+    base = ctype.replace("const", "").strip()
+    return _CTYPE[base]
+
+
+def declarations():
+    global _decls
+    if _decls is None:
+        _decls = parse_header()
+    return _decls
+
+
+def lib():
+    """Load and bind the HIP library (raises if it is absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()')"
+            )
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (ret, params) in declarations().items():
+            fn = getattr(L, name)
+            fn.argtypes = [_argtype(t) for t, _ in params]
+            fn.restype = {"int": ctypes.c_int, "size_t": ctypes.c_size_t}.get(ret, ctypes.c_char_p)
+        _lib = L
+    return _lib
+
+
+class CullavoError(RuntimeError):
+    pass
+
+
+def call(name: str, *args) -> int:
+    """Invoke cullavo_<name>; raise CullavoError with cullavo_last_error() on failure."""
+    L = lib()
+    rc = getattr(L, "cullavo_" + name)(*args)
+    if rc != 0:
+        msg = L.cullavo_last_error().decode(errors="replace")
+        if rc == 1:
+            raise ValueError(f"cullavo_{name}: {msg}")
+        raise CullavoError(f"cullavo_{name} failed (code {rc}): {msg}")
+    return rc

@@ -1,0 +1,591 @@
+// Flash attention forward/backward for gfx950 (v_mfma_f32_32x32x16_bf16).
+//
+// Replaces the LM's causal attention (FA2 in the reference: cullavo/load_cullavo.py:72;
+// arithmetic of tf:llama/modeling_llama.py:191-214, scale 1/sqrt(128)) and CLIP's non-causal
+// attention (tf:clip/modeling_clip.py:280-336, scale 1/8). Tensors are [B, L, H, D] with a
+// token stride, i.e. the q/k/v projection outputs are consumed in place.
+//
+// Forward: a wave owns 32 query rows; the 4 waves of a workgroup share 64-key K/V tiles in
+// LDS (double-buffered, register-staged, one barrier per tile). Scores are computed swapped,
+// S^T = K Q^T, so every lane owns one query row: the online-softmax row max/sum is 32 register
+// ops plus one cross-half shuffle, P^T feeds the P·V MFMA straight from the accumulator
+// registers (O^T = V^T P^T) and V^T fragments come from ds_read_b64_tr_b16 transposed reads.
+// Backward: kernel A (per 32-key slice per wave: dV = P^T dO, dK = dS^T Q) and kernel B (per
+// 32-query slice: dQ = dS K), both recomputing P from the saved log-sum-exp; no atomics, so
+// results are bitwise reproducible.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 frag8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// LDS image of a [rows][D] bf16 tile, 16-byte chunk ch of row r. D=128: the dual-use XOR
+// image (conflict-free for both the row reads and the tr16 reads, cdna_hip_programming.md
+// T10 (b)); D=64: chunk ^ ((r>>1)&7) (row reads conflict-free, tr reads 2-way).
+template <int D>
+DEV int kv_off(int r, int ch) {
+  if (D == 128) return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+  return 128 * r + 16 * (ch ^ ((r >> 1) & 7));
+}
+
+// row fragment for a 32x32x16 operand: lane holds T[rbase + (lane&31)][16s + 8h + j]
+template <int D>
+DEV frag8 row_frag(const char* lds, int rbase, int s, int lane) {
+  const int r = rbase + (lane & 31), ch = 2 * s + (lane >> 5);
+  return __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(lds + kv_off<D>(r, ch)));
+}
+
+// transposed fragment: lane holds T[kb + 8(j>>2) + 4h + (j&3)][d0 + (lane&31)], j = 0..7
+// (the k order of an accumulator tile used as the other MFMA operand, guide §3)
+template <int D>
+DEV frag8 tr_frag(const char* lds, int kb, int d0, int lane) {
+  const int h = lane >> 5, i = lane & 15, q = i >> 2, p = i & 3;
+  const int dcol = d0 + 16 * ((lane >> 4) & 1);
+  const int ch = (dcol >> 3) + (p >> 1);
+  const int r0 = kb + 4 * h + q;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + kv_off<D>(r0, ch) + 8 * (p & 1)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + kv_off<D>(r0 + 8, ch) + 8 * (p & 1)));
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(frag8, v);
+}
+
+// accumulator registers 8s..8s+7 of a 32x32 tile -> bf16 operand fragment
+DEV frag8 pack_frag(const f32x16& a, int s) {
+  frag8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (__bf16)a[8 * s + j];
+  return f;
+}
+
+// global -> registers -> LDS staging of a [ROWS][D] tile of a [L, H, D]-strided tensor
+template <int ROWS, int D>
+struct Stage {
+  static constexpr int kChunks = ROWS * D / 8;
+  static constexpr int kPer = kChunks / 256;  // 16-byte chunks per thread
+  u16x8 r[kPer];
+  DEV void load(const u16* base, int64_t ld, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      const int row = q / (D / 8), ch = q % (D / 8);
+      r[i] = (row0 + row < nrows) ? *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + row) * ld + ch * 8)
+                                  : u16x8(0);
+    }
+  }
+  DEV void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      const int row = q / (D / 8), ch = q % (D / 8);
+      *reinterpret_cast<u16x8*>(lds + kv_off<D>(row, ch)) = r[i];
+    }
+  }
+};
+
+// row of accumulator register r of a 32x32 tile for lane half h
+DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ============================================================================================
+// forward
+// ============================================================================================
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, int64_t ldq,
+                                                     const u16* __restrict__ K, int64_t ldk,
+                                                     const u16* __restrict__ V, int64_t ldv,
+                                                     u16* __restrict__ O, int64_t ldo,
+                                                     float* __restrict__ LSE, int H, int Lq, int Lk,
+                                                     float scale, const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 64;                 // keys per tile
+  constexpr int TILE = KT * D * 2;       // bytes per K (or V) tile
+  constexpr int NS = D / 16;             // k-steps over D
+  constexpr int ND = D / 32;             // O^T tiles
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heavy causal blocks first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int q = qb * 128 + wave * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+
+  frag8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    u16x8 v = (q < Lq) ? *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ldq + 16 * s + 8 * hf) : u16x8(0);
+    qf[s] = __builtin_bit_cast(frag8, v);
+  }
+
+  f32x16 o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) o[i] = f32x16(0.f);
+  float m = -INFINITY, l = 0.f;
+  const float c = scale * kLog2e;
+
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * 128 + 128);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  Stage<KT, D> sk, sv;
+  // buffer i: K at smem + 2*i*TILE, V right after it
+#define bufK(i) (smem + 2 * (i) * TILE)
+#define bufV(i) (smem + 2 * (i) * TILE + TILE)
+  if (t0 < ntiles) {
+    sk.load(Kb, ldk, t0 * KT, Lk);
+    sv.load(Vb, ldv, t0 * KT, Lk);
+    sk.store(bufK(0));
+    sv.store(bufV(0));
+  }
+  __syncthreads();
+
+  for (int t = t0; t < ntiles; ++t) {
+    const int cur = (t - t0) & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ldk, (t + 1) * KT, Lk);
+      sv.load(Vb, ldv, (t + 1) * KT, Lk);
+    }
+    // S^T = K Q^T for two 32-key halves
+    f32x16 st[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      st[kt] = f32x16(0.f);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufK(cur), kt * 32, s, lane), qf[s], st[kt], 0, 0, 0);
+    }
+    // scale, mask, tile max
+    float tmax = -INFINITY;
+    const int kbase = t * KT;
+    const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = st[kt][r] * c;
+        if (need_mask) {
+          const int key = kbase + kt * 32 + acc_row(r, hf);
+          if (key >= Lk || key < kstart || (CAUSAL && key > q)) v = -INFINITY;
+        }
+        st[kt][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(m, tmax);
+    const float muse = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = exp2f(m - muse);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = exp2f(st[kt][r] - muse);
+        st[kt][r] = pv;
+        rs += pv;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mnew;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) o[i] *= alpha;
+    // O^T += V^T P^T
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const frag8 pf = pack_frag(st[kt], s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bufV(cur), kt * 32 + 16 * s, dt * 32, lane), pf, o[dt], 0, 0, 0);
+      }
+    if (more) {
+      sk.store(bufK(cur ^ 1));
+      sv.store(bufV(cur ^ 1));
+    }
+    __syncthreads();
+  }
+
+  if (q < Lq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    u16* Ob = O + ((int64_t)b * Lq + q) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][rr * 4 + j] * inv);
+        *reinterpret_cast<u16x4*>(Ob + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+    if (hf == 0) LSE[((int64_t)b * H + h) * Lq + q] = l > 0.f ? (m + log2f(l)) * kLn2 : INFINITY;
+  }
+}
+
+// ============================================================================================
+// backward
+// ============================================================================================
+// delta[b,h,q] = sum_d dO*O  (f32); one 16-lane group per (token, head) row for D=128
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta_k(const u16* __restrict__ O, int64_t ldo,
+                                                    const u16* __restrict__ dO, int64_t lddo,
+                                                    float* __restrict__ delta, int B, int H, int L) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;  // (b, t, h) row
+  const int sub = threadIdx.x % LPR;
+  const int64_t nrows = (int64_t)B * L * H;
+  float acc = 0.f;
+  if (row < nrows) {
+    const int hh = (int)(row % H);
+    const int64_t bt = row / H;
+    float a[8], d[8];
+    load8(O + bt * ldo + (int64_t)hh * D + sub * 8, a);
+    load8(dO + bt * lddo + (int64_t)hh * D + sub * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * d[j];
+  }
+#pragma unroll
+  for (int o = LPR / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (row < nrows && sub == 0) {
+    const int hh = (int)(row % H);
+    const int64_t bt = row / H;
+    const int64_t bb = bt / L, t = bt % L;
+    delta[(bb * H + hh) * L + t] = acc;
+  }
+}
+
+// Kernel A: dK, dV. A wave owns 32 keys (K, V fragments in registers); the workgroup sweeps
+// 32-row query tiles staged in LDS. S = Q K^T and dP = dO V^T keep the key on the lane;
+// dV = P^T dO and dK = dS^T Q take P / dS straight from the accumulators (A operand) and
+// dO / Q as transposed LDS fragments.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
+    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
+    const int32_t* __restrict__ kv_start) {
+  constexpr int QT = 32;
+  constexpr int TILE = QT * D * 2;
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // [buf][Q tile | dO tile | lse(32 f32) | delta(32 f32)]
+  constexpr int BUF = 2 * TILE + 2 * QT * 4;
+
+  const int nkb = gridDim.x;
+  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;
+  (void)nkb;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int key = kb * 128 + wave * 32 + (lane & 31);  // this lane's key (operand column)
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
+  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
+
+  frag8 kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const bool ok = key < Lk;
+    kf[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Kb + (int64_t)key * ldk + 16 * s + 8 * hf) : u16x8(0));
+    vf[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Vb + (int64_t)key * ldv + 16 * s + 8 * hf) : u16x8(0));
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dk[i] = f32x16(0.f); dv[i] = f32x16(0.f); }
+  const float c = scale * kLog2e;
+
+  // query tiles that can see this block's keys
+  const int kmin = kb * 128;
+  int qt0 = CAUSAL ? (kmin / QT) : 0;
+  const int nqt = (Lq + QT - 1) / QT;
+  const bool block_live = kmin < Lk && (kmin + 128 > kstart);
+
+  Stage<QT, D> sq, sdo;
+  auto stage_aux = [&](char* buf, int qt) {  // lse / delta for 32 rows (threads 0..63)
+    if (threadIdx.x < 64) {
+      const int r = threadIdx.x & 31;
+      const int qq = qt * QT + r;
+      float* dst = (float*)(buf + 2 * TILE) + (threadIdx.x >> 5) * QT + r;
+      const float val = (threadIdx.x < 32) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+      *dst = val;
+    }
+  };
+  if (block_live && qt0 < nqt) {
+    sq.load(Qb, ldq, qt0 * QT, Lq);
+    sdo.load(dOb, lddo, qt0 * QT, Lq);
+    sq.store(smem);
+    sdo.store(smem + TILE);
+    stage_aux(smem, qt0);
+  }
+  __syncthreads();
+
+  for (int qt = qt0; block_live && qt < nqt; ++qt) {
+    const int cur = (qt - qt0) & 1;
+    char* buf = smem + cur * BUF;
+    char* nbuf = smem + (cur ^ 1) * BUF;
+    const bool more = qt + 1 < nqt;
+    if (more) {
+      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
+      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+    }
+    const float* slse = (const float*)(buf + 2 * TILE);
+    const float* sdel = slse + QT;
+    // S[q][key], dP[q][key]
+    f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 0, s, lane), kf[s], sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TILE, 0, s, lane), vf[s], pacc, 0, 0, 0);
+    }
+    // P = exp(S*scale - lse), dS = P * (dP - delta)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 8 * rr + 4 * hf);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 8 * rr + 4 * hf);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = rr * 4 + j;
+        const int qq = qt * QT + 8 * rr + 4 * hf + j;
+        float pv = exp2f(sacc[r] * c - l4[j] * kLog2e);
+        if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
+        sacc[r] = pv;
+        pacc[r] = pv * (pacc[r] - d4[j]);
+      }
+    }
+    // dV += P^T dO ; dK += dS^T Q   (A operand = accumulator, B = transposed LDS fragment)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8 pf = pack_frag(sacc, s);
+      const frag8 df = pack_frag(pacc, s);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TILE, 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_frag<D>(buf, 16 * s, dt * 32, lane), dk[dt], 0, 0, 0);
+      }
+    }
+    if (more) {
+      sq.store(nbuf);
+      sdo.store(nbuf + TILE);
+      stage_aux(nbuf, qt + 1);
+    }
+    __syncthreads();
+  }
+
+  // dK/dV[key][d]: register r = key row, lane = d column
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kk = kb * 128 + wave * 32 + acc_row(r, hf);
+      if (kk < Lk) {
+        const int d = dt * 32 + (lane & 31);
+        dK[((int64_t)b * Lk + kk) * lddk + (int64_t)h * D + d] = f2bf(dk[dt][r] * scale);
+        dV[((int64_t)b * Lk + kk) * lddv + (int64_t)h * D + d] = f2bf(dv[dt][r]);
+      }
+    }
+}
+
+// Kernel B: dQ. A wave owns 32 query rows (Q, dO fragments in registers, lse/delta per
+// lane); the workgroup sweeps 32-key K/V tiles. S^T = K Q^T, dP^T = V dO^T (query on the
+// lane), dQ^T += K^T dS^T with K^T as a transposed LDS fragment.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dQ,
+    int64_t lddq, int H, int Lq, int Lk, float scale, const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 32;
+  constexpr int TILE = KT * D * 2;
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = gridDim.x;
+  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int q = qb * 128 + wave * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+
+  frag8 qf[NS], of[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const bool ok = q < Lq;
+    qf[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ldq + 16 * s + 8 * hf) : u16x8(0));
+    of[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(dOb + (int64_t)q * lddo + 16 * s + 8 * hf) : u16x8(0));
+  }
+  const float lse2 = (q < Lq) ? LSE[((int64_t)b * H + h) * Lq + q] * kLog2e : INFINITY;
+  const float del = (q < Lq) ? DELTA[((int64_t)b * H + h) * Lq + q] : 0.f;
+  const float c = scale * kLog2e;
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = f32x16(0.f);
+
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * 128 + 128);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  Stage<KT, D> sk, sv;
+  // buffer i: K at smem + 2*i*TILE, V right after it
+#define bufK(i) (smem + 2 * (i) * TILE)
+#define bufV(i) (smem + 2 * (i) * TILE + TILE)
+  if (t0 < ntiles) {
+    sk.load(Kb, ldk, t0 * KT, Lk);
+    sv.load(Vb, ldv, t0 * KT, Lk);
+    sk.store(bufK(0));
+    sv.store(bufV(0));
+  }
+  __syncthreads();
+  for (int t = t0; t < ntiles; ++t) {
+    const int cur = (t - t0) & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ldk, (t + 1) * KT, Lk);
+      sv.load(Vb, ldv, (t + 1) * KT, Lk);
+    }
+    f32x16 st = f32x16(0.f), dpt = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufK(cur), 0, s, lane), qf[s], st, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufV(cur), 0, s, lane), of[s], dpt, 0, 0, 0);
+    }
+    const int kbase = t * KT;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kbase + acc_row(r, hf);
+      float pv = exp2f(st[r] * c - lse2);
+      if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
+      dpt[r] = pv * (dpt[r] - del);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8 df = pack_frag(dpt, s);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bufK(cur), 16 * s, dt * 32, lane), df, dq[dt], 0, 0, 0);
+    }
+    if (more) {
+      sk.store(bufK(cur ^ 1));
+      sv.store(bufV(cur ^ 1));
+    }
+    __syncthreads();
+  }
+  if (q < Lq) {
+    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[dt][rr * 4 + j] * scale);
+        *reinterpret_cast<u16x4*>(dQb + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+  }
+}
+
+template <typename Kern>
+void set_smem(Kern k, int bytes) {
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+template <int D, bool CAUSAL>
+int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, u16* o,
+               int64_t ldo, float* lse, int B, int H, int Lq, int Lk, float scale, const int32_t* ks,
+               hipStream_t s) {
+  const int smem = 4 * 64 * D * 2;
+  static bool once = false;
+  if (!once) { set_smem(attn_fwd_k<D, CAUSAL>, smem); once = true; }
+  dim3 grid((unsigned)cdiv(Lq, 128), H, B);
+  attn_fwd_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  return cullavo_check_launch("attn_fwd");
+}
+
+template <int D, bool CAUSAL>
+int bwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
+               int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
+               u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
+               const int32_t* ks, hipStream_t s) {
+  const int64_t rows = (int64_t)B * Lq * H;
+  attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
+  const int smem_a = 2 * (2 * 32 * D * 2 + 2 * 32 * 4);
+  const int smem_b = 4 * 32 * D * 2;
+  static bool once = false;
+  if (!once) {
+    set_smem(attn_bwd_dkdv_k<D, CAUSAL>, smem_a);
+    set_smem(attn_bwd_dq_k<D, CAUSAL>, smem_b);
+    once = true;
+  }
+  dim3 ga((unsigned)cdiv(Lk, 128), H, B);
+  attn_bwd_dkdv_k<D, CAUSAL><<<ga, 256, smem_a, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk,
+                                                      dv, lddv, H, Lq, Lk, scale, ks);
+  dim3 gb((unsigned)cdiv(Lq, 128), H, B);
+  attn_bwd_dq_k<D, CAUSAL><<<gb, 256, smem_b, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H,
+                                                    Lq, Lk, scale, ks);
+  return cullavo_check_launch("attn_bwd");
+}
+
+}  // namespace
+
+extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                int64_t ldv, void* o, int64_t ldo, float* lse, int B, int H, int Lq, int Lk,
+                                int D, float scale, int causal, const int32_t* kv_start, int dtype,
+                                void* stream) {
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "attention is bf16 only");
+  CV_REQUIRE(D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 64 or 128");
+  CV_REQUIRE(!causal || Lq == Lk, CULLAVO_EINVAL, "causal attention needs Lq == Lk");
+  CV_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0, CULLAVO_EINVAL, "token strides must be multiples of 8");
+  CV_REQUIRE(ldq >= (int64_t)H * D && ldk >= (int64_t)H * D && ldv >= (int64_t)H * D && ldo >= (int64_t)H * D,
+             CULLAVO_EINVAL, "token stride smaller than H*D");
+  if (B == 0 || H == 0 || Lq == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v;
+  u16* O = (u16*)o;
+  if (D == 128)
+    return causal ? fwd_launch<128, true>(Q, ldq, K, ldk, V, ldv, O, ldo, lse, B, H, Lq, Lk, scale, kv_start, s)
+                  : fwd_launch<128, false>(Q, ldq, K, ldk, V, ldv, O, ldo, lse, B, H, Lq, Lk, scale, kv_start, s);
+  return causal ? fwd_launch<64, true>(Q, ldq, K, ldk, V, ldv, O, ldo, lse, B, H, Lq, Lk, scale, kv_start, s)
+                : fwd_launch<64, false>(Q, ldq, K, ldk, V, ldv, O, ldo, lse, B, H, Lq, Lk, scale, kv_start, s);
+}
+
+extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                                const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
+                                int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
+                                float scale, int causal, const int32_t* kv_start, int dtype, void* stream) {
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "attention is bf16 only");
+  CV_REQUIRE(D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 64 or 128");
+  CV_REQUIRE(!causal || Lq == Lk, CULLAVO_EINVAL, "causal attention needs Lq == Lk");
+  CV_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 && lddq % 8 == 0 &&
+                 lddk % 8 == 0 && lddv % 8 == 0,
+             CULLAVO_EINVAL, "token strides must be multiples of 8");
+  if (B == 0 || H == 0 || Lq == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v, *O = (const u16*)o, *dO = (const u16*)dout;
+  u16 *dQ = (u16*)dq, *dK = (u16*)dk, *dV = (u16*)dv;
+#define BWD(DD, CC) bwd_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+  if (D == 128) return causal ? BWD(128, true) : BWD(128, false);
+  return causal ? BWD(64, true) : BWD(64, false);
+#undef BWD
+}

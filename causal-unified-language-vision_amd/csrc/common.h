@@ -1,0 +1,95 @@
+// Shared device helpers for the CuLLaVO gfx950 kernels: bf16 conversion, vector types,
+// wave (64-lane) reductions and the C-ABI error plumbing.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <algorithm>
+
+#include "../../include/cullavo_capi.h"
+
+typedef unsigned short u16;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;  // 8 bf16 = 16 B
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;  // 4 bf16 = 8 B
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+#define DEV __device__ __forceinline__
+
+DEV float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+// round-to-nearest-even through the native type (v_cvt_pk_bf16_f32 on gfx950; NaN stays NaN)
+DEV u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+DEV float round_bf(float f) { return bf2f(f2bf(f)); }
+
+template <typename T> struct Elt;
+template <> struct Elt<u16> {
+  static DEV float ld(const u16* p, int64_t i) { return bf2f(p[i]); }
+  static DEV void st(u16* p, int64_t i, float v) { p[i] = f2bf(v); }
+  static DEV float rnd(float v) { return round_bf(v); }
+};
+template <> struct Elt<float> {
+  static DEV float ld(const float* p, int64_t i) { return p[i]; }
+  static DEV void st(float* p, int64_t i, float v) { p[i] = v; }
+  static DEV float rnd(float v) { return v; }
+};
+
+// load/store 8 consecutive elements as f32
+DEV void load8(const u16* p, float* v) {
+  u16x8 x = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(x[j]);
+}
+DEV void load8(const float* p, float* v) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+DEV void store8(u16* p, const float* v) {
+  u16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = f2bf(v[j]);
+  *reinterpret_cast<u16x8*>(p) = x;
+}
+DEV void store8(float* p, const float* v) {
+  f32x4 a, b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
+  *reinterpret_cast<f32x4*>(p) = a;
+  *reinterpret_cast<f32x4*>(p + 4) = b;
+}
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---- host-side error plumbing ------------------------------------------------------------
+void cullavo_set_error(const std::string& msg);
+int cullavo_check_launch(const char* what);
+
+#define CV_REQUIRE(cond, code, msg)                  \
+  do {                                               \
+    if (!(cond)) {                                   \
+      cullavo_set_error(std::string(__func__) + ": " + (msg)); \
+      return (code);                                 \
+    }                                                \
+  } while (0)
+
+#define CV_STREAM(s) (reinterpret_cast<hipStream_t>(s))
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

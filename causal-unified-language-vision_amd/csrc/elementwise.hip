@@ -1,0 +1,364 @@
+// Element-wise and small-reduction kernels of the CuLLaVO step: SwiGLU, activation backward,
+// bias-gradient column sums, Llama RoPE, and the optimiser pieces (sum of squares, clip
+// coefficient, fused AdamW). All HBM-bound: 16 B per lane per access, grid-stride loops.
+#include "common.h"
+
+namespace {
+
+constexpr int kEwBlocks = 2048;  // grid cap for streaming kernels (256 CUs x 8)
+
+DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+DEV float siluf_(float x) { return x / (1.f + __expf(-x)); }
+
+int ew_grid(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(kEwBlocks, cdiv(nvec, 256))); }
+
+// ---- SwiGLU (tf:llama/modeling_llama.py:163-176: down(act(gate(x)) * up(x))) --------------
+// gu: fused gate|up projection output [rows, 2F]; one 8-wide column group per thread
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, int64_t rows, int64_t F,
+                                                    T* __restrict__ o) {
+  const int64_t fv = F / 8, nvec = rows * fv;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / fv, c = (i % fv) * 8;
+    float gv[8], uv[8], ov[8];
+    load8(gu + r * 2 * F + c, gv);
+    load8(gu + r * 2 * F + F + c, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ov[j] = Elt<T>::rnd(siluf_(gv[j])) * uv[j];
+    store8(o + r * F + c, ov);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ d, const T* __restrict__ gu,
+                                                    int64_t rows, int64_t F, T* __restrict__ dgu) {
+  const int64_t fv = F / 8, nvec = rows * fv;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / fv, c = (i % fv) * 8;
+    float dv[8], gv[8], uv[8], a[8], b[8];
+    load8(d + r * F + c, dv);
+    load8(gu + r * 2 * F + c, gv);
+    load8(gu + r * 2 * F + F + c, uv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sigmoidf_(gv[j]);
+      const float silu = gv[j] * s;
+      b[j] = dv[j] * Elt<T>::rnd(silu);
+      a[j] = dv[j] * uv[j] * s * (1.f + gv[j] * (1.f - s));
+    }
+    store8(dgu + r * 2 * F + c, a);
+    store8(dgu + r * 2 * F + F + c, b);
+  }
+}
+
+// ---- activation backward (projector GELU, CLIP quick_gelu) ---------------------------------
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void act_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                 T* __restrict__ dx, int64_t nvec) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float dv[8], xv[8], o[8];
+    load8(dy + i * 8, dv);
+    load8(x + i * 8, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = xv[j];
+      float dg;
+      if (ACT == CULLAVO_ACT_GELU) {
+        const float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+        const float pdf = 0.39894228040143268f * __expf(-0.5f * v * v);
+        dg = cdf + v * pdf;
+      } else {
+        const float s = sigmoidf_(1.702f * v);
+        dg = s + 1.702f * v * s * (1.f - s);
+      }
+      o[j] = dv[j] * dg;
+    }
+    store8(dx + i * 8, o);
+  }
+}
+
+// ---- column sums (bias gradients) ----------------------------------------------------------
+// block: 32 column groups of 8 columns x 8 row lanes; grid.y splits the rows.
+constexpr int kColsumSplit = 32;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_k(const T* __restrict__ x, int64_t rows, int64_t cols,
+                                                float* __restrict__ part) {
+  __shared__ float red[8][256 + 8];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int64_t c0 = (int64_t)blockIdx.x * 256 + cg * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < cols) {
+    for (int64_t r = rl + 8 * blockIdx.y; r < rows; r += 8 * gridDim.y) {
+      float v[8];
+      load8(x + r * cols + c0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cg * 8 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of this block
+  const int64_t col = (int64_t)blockIdx.x * 256 + c;
+  if (col < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][c];
+    part[(int64_t)blockIdx.y * cols + col] = s;
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void colsum_final_k(const float* __restrict__ part, int nsplit,
+                                                      int64_t cols, TO* __restrict__ out, float beta) {
+  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < nsplit; ++p) s += part[(int64_t)p * cols + col];
+  if (beta != 0.f) s += beta * Elt<TO>::ld(out, col);
+  Elt<TO>::st(out, col, s);
+}
+
+// ---- RoPE (tf:llama/modeling_llama.py:73-160) ----------------------------------------------
+// one block per token; thread = (head slot, group of 4 frequency indices). cos/sin are
+// computed in f32 from pos * inv_freq and rounded to the activation dtype (reference :121-125);
+// out = rnd(rnd(x*cos) + rnd(rotate_half(x)*sin)), rotate_half(x) = cat(-x2, x1).
+template <typename T>
+DEV void rope_heads(T* base, int64_t ld, int nh, int half, int i4, int hslot, int nslot,
+                    const float* c, const float* s, int inverse) {
+  for (int h = hslot; h < nh; h += nslot) {
+    T* p1 = base + (int64_t)h * 2 * half + i4 * 4;
+    T* p2 = p1 + half;
+    float x1[4], x2[4], o1[4], o2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x1[j] = Elt<T>::ld(p1, j);
+      x2[j] = Elt<T>::ld(p2, j);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!inverse) {
+        o1[j] = Elt<T>::rnd(Elt<T>::rnd(x1[j] * c[j]) + Elt<T>::rnd(-x2[j] * s[j]));
+        o2[j] = Elt<T>::rnd(Elt<T>::rnd(x2[j] * c[j]) + Elt<T>::rnd(x1[j] * s[j]));
+      } else {  // transpose rotation: the gradient of the forward map
+        o1[j] = x1[j] * c[j] + x2[j] * s[j];
+        o2[j] = x2[j] * c[j] - x1[j] * s[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Elt<T>::st(p1, j, o1[j]);
+      Elt<T>::st(p2, j, o2[j]);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rope_k(T* __restrict__ q, int64_t ldq, T* __restrict__ k,
+                                              int64_t ldk, const int64_t* __restrict__ pos, int hq,
+                                              int hk, int D, float theta, int inverse) {
+  const int64_t t = blockIdx.x;
+  const int half = D / 2;
+  const int ng = half / 4;  // groups of 4 frequencies per head
+  const int i4 = threadIdx.x % ng;
+  const int hslot = threadIdx.x / ng;
+  const int nslot = 256 / ng;
+  const float p = (float)pos[t];
+  float c[4], s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = i4 * 4 + j;
+    const float inv_freq = 1.0f / powf(theta, (float)(2 * i) / (float)D);
+    const float ang = p * inv_freq;
+    c[j] = Elt<T>::rnd(cosf(ang));
+    s[j] = Elt<T>::rnd(sinf(ang));
+  }
+  if (hslot >= nslot) return;
+  rope_heads<T>(q + t * ldq, ldq, hq, half, i4, hslot, nslot, c, s, inverse);
+  if (k != nullptr) rope_heads<T>(k + t * ldk, ldk, hk, half, i4, hslot, nslot, c, s, inverse);
+}
+
+// ---- optimiser ------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t nvec = n / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j] * v[j];
+  }
+  if (blockIdx.x == 0) {  // tail
+    for (int64_t i = nvec * 8 + threadIdx.x; i < n; i += 256) {
+      const float v = Elt<T>::ld(x, i);
+      acc += v * v;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void clip_coef_k(const float* sumsq, float max_norm, float* coef, float* norm_out) {
+  const float norm = sqrtf(sumsq[0]);
+  if (norm_out) norm_out[0] = norm;
+  coef[0] = fminf(1.f, max_norm / (norm + 1e-6f));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void scale_k(T* __restrict__ x, int64_t n, const float* __restrict__ sc) {
+  const float s = sc[0];
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    Elt<T>::st(x, i, Elt<T>::ld(x, i) * s);
+}
+
+// torch.optim.AdamW (single-tensor math): p *= 1-lr*wd; m = lerp(m, g, 1-b1);
+// v = b2*v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+template <typename T, typename S>
+__global__ __launch_bounds__(256) void adamw_k(T* __restrict__ p, const T* __restrict__ g,
+                                               S* __restrict__ m, S* __restrict__ v, int64_t n,
+                                               float lr, float b1, float b2, float eps, float wd,
+                                               float bc1, float bc2_sqrt,
+                                               const float* __restrict__ gscale) {
+  const float gs = gscale ? gscale[0] : 1.f;
+  const float step_size = lr / bc1;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gv = Elt<T>::ld(g, i) * gs;
+    float pv = Elt<T>::ld(p, i);
+    float mv = Elt<S>::ld(m, i);
+    float vv = Elt<S>::ld(v, i);
+    pv = Elt<T>::rnd(pv * (1.f - lr * wd));
+    mv = Elt<S>::rnd(mv + (gv - mv) * (1.f - b1));
+    vv = Elt<S>::rnd(vv * b2 + (1.f - b2) * gv * gv);
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pv = pv - step_size * mv / denom;
+    Elt<T>::st(p, i, pv);
+    Elt<S>::st(m, i, mv);
+    Elt<S>::st(v, i, vv);
+  }
+}
+
+}  // namespace
+
+extern "C" int cullavo_swiglu_fwd(const void* gu, int64_t rows, int64_t F, void* out, int dtype,
+                                  void* stream) {
+  CV_REQUIRE(F % 8 == 0, CULLAVO_EINVAL, "F must be a multiple of 8");
+  if (rows == 0 || F == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int g = ew_grid(rows * F / 8);
+  if (dtype == CULLAVO_DT_BF16) swiglu_fwd_k<u16><<<g, 256, 0, s>>>((const u16*)gu, rows, F, (u16*)out);
+  else if (dtype == CULLAVO_DT_F32) swiglu_fwd_k<float><<<g, 256, 0, s>>>((const float*)gu, rows, F, (float*)out);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  return cullavo_check_launch("swiglu_fwd");
+}
+
+extern "C" int cullavo_swiglu_bwd(const void* dout, const void* gu, int64_t rows, int64_t F, void* dgu,
+                                  int dtype, void* stream) {
+  CV_REQUIRE(F % 8 == 0, CULLAVO_EINVAL, "F must be a multiple of 8");
+  if (rows == 0 || F == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int g = ew_grid(rows * F / 8);
+  if (dtype == CULLAVO_DT_BF16) swiglu_bwd_k<u16><<<g, 256, 0, s>>>((const u16*)dout, (const u16*)gu, rows, F, (u16*)dgu);
+  else if (dtype == CULLAVO_DT_F32) swiglu_bwd_k<float><<<g, 256, 0, s>>>((const float*)dout, (const float*)gu, rows, F, (float*)dgu);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  return cullavo_check_launch("swiglu_bwd");
+}
+
+extern "C" int cullavo_act_bwd(int act, const void* dy, const void* preact, void* dx, int64_t n,
+                               int dtype, void* stream) {
+  CV_REQUIRE(n % 8 == 0, CULLAVO_EINVAL, "n must be a multiple of 8");
+  CV_REQUIRE(act == CULLAVO_ACT_GELU || act == CULLAVO_ACT_QUICK_GELU, CULLAVO_EINVAL, "act");
+  if (n == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int64_t nv = n / 8;
+  const int g = ew_grid(nv);
+  if (dtype == CULLAVO_DT_BF16) {
+    if (act == CULLAVO_ACT_GELU) act_bwd_k<u16, CULLAVO_ACT_GELU><<<g, 256, 0, s>>>((const u16*)dy, (const u16*)preact, (u16*)dx, nv);
+    else act_bwd_k<u16, CULLAVO_ACT_QUICK_GELU><<<g, 256, 0, s>>>((const u16*)dy, (const u16*)preact, (u16*)dx, nv);
+  } else if (dtype == CULLAVO_DT_F32) {
+    if (act == CULLAVO_ACT_GELU) act_bwd_k<float, CULLAVO_ACT_GELU><<<g, 256, 0, s>>>((const float*)dy, (const float*)preact, (float*)dx, nv);
+    else act_bwd_k<float, CULLAVO_ACT_QUICK_GELU><<<g, 256, 0, s>>>((const float*)dy, (const float*)preact, (float*)dx, nv);
+  } else {
+    CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  }
+  return cullavo_check_launch("act_bwd");
+}
+
+extern "C" size_t cullavo_colsum_workspace(int64_t rows, int64_t cols) {
+  (void)rows;
+  return (size_t)kColsumSplit * cols * sizeof(float);
+}
+
+extern "C" int cullavo_colsum(const void* x, int64_t rows, int64_t cols, void* out, int out_dtype,
+                              float beta, float* ws, int dtype, void* stream) {
+  CV_REQUIRE(cols % 8 == 0, CULLAVO_EINVAL, "cols must be a multiple of 8");
+  CV_REQUIRE(ws != nullptr, CULLAVO_EINVAL, "workspace required");
+  if (cols == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  dim3 grid((unsigned)cdiv(cols, 256), kColsumSplit);
+  if (dtype == CULLAVO_DT_BF16) colsum_k<u16><<<grid, 256, 0, s>>>((const u16*)x, rows, cols, ws);
+  else if (dtype == CULLAVO_DT_F32) colsum_k<float><<<grid, 256, 0, s>>>((const float*)x, rows, cols, ws);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  if (out_dtype == CULLAVO_DT_BF16) colsum_final_k<u16><<<cdiv(cols, 256), 256, 0, s>>>(ws, kColsumSplit, cols, (u16*)out, beta);
+  else colsum_final_k<float><<<cdiv(cols, 256), 256, 0, s>>>(ws, kColsumSplit, cols, (float*)out, beta);
+  return cullavo_check_launch("colsum");
+}
+
+extern "C" int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const int64_t* position_ids,
+                            int64_t tokens, int hq, int hk, int head_dim, float theta, int inverse,
+                            int dtype, void* stream) {
+  CV_REQUIRE(head_dim % 8 == 0 && head_dim >= 8 && head_dim / 8 <= 256, CULLAVO_EINVAL, "head_dim");
+  if (tokens == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  if (dtype == CULLAVO_DT_BF16) rope_k<u16><<<(unsigned)tokens, 256, 0, s>>>((u16*)q, ldq, (u16*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
+  else if (dtype == CULLAVO_DT_F32) rope_k<float><<<(unsigned)tokens, 256, 0, s>>>((float*)q, ldq, (float*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  return cullavo_check_launch("rope");
+}
+
+extern "C" int cullavo_sumsq(const void* x, int64_t n, float* out, int dtype, void* stream) {
+  if (n == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int g = ew_grid(n / 8 + 1);
+  if (dtype == CULLAVO_DT_BF16) sumsq_k<u16><<<g, 256, 0, s>>>((const u16*)x, n, out);
+  else if (dtype == CULLAVO_DT_F32) sumsq_k<float><<<g, 256, 0, s>>>((const float*)x, n, out);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  return cullavo_check_launch("sumsq");
+}
+
+extern "C" int cullavo_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out,
+                                 void* stream) {
+  clip_coef_k<<<1, 1, 0, CV_STREAM(stream)>>>(sumsq, max_norm, coef, norm_out);
+  return cullavo_check_launch("clip_coef");
+}
+
+extern "C" int cullavo_scale_inplace(void* x, int64_t n, const float* scale, int dtype, void* stream) {
+  if (n == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  if (dtype == CULLAVO_DT_BF16) scale_k<u16><<<ew_grid(n), 256, 0, s>>>((u16*)x, n, scale);
+  else if (dtype == CULLAVO_DT_F32) scale_k<float><<<ew_grid(n), 256, 0, s>>>((float*)x, n, scale);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  return cullavo_check_launch("scale_inplace");
+}
+
+extern "C" int cullavo_adamw(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
+                             float lr, float beta1, float beta2, float eps, float weight_decay,
+                             int64_t step, const float* grad_scale, int dtype, int state_dtype,
+                             void* stream) {
+  CV_REQUIRE(step >= 1, CULLAVO_EINVAL, "step must be >= 1");
+  if (n == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const float bc1 = 1.f - (float)std::pow((double)beta1, (double)step);
+  const float bc2s = (float)std::sqrt(1.0 - std::pow((double)beta2, (double)step));
+  const int g = ew_grid(n);
+#define ADAM(T, S) adamw_k<T, S><<<g, 256, 0, s>>>((T*)param, (const T*)grad, (S*)exp_avg, (S*)exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale)
+  if (dtype == CULLAVO_DT_BF16 && state_dtype == CULLAVO_DT_BF16) ADAM(u16, u16);
+  else if (dtype == CULLAVO_DT_BF16 && state_dtype == CULLAVO_DT_F32) ADAM(u16, float);
+  else if (dtype == CULLAVO_DT_F32 && state_dtype == CULLAVO_DT_F32) ADAM(float, float);
+  else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype combination");
+#undef ADAM
+  return cullavo_check_launch("adamw");
+}

@@ -1,0 +1,289 @@
+// bf16 MFMA GEMM with fused epilogues for every Linear of the CuLLaVO step (forward, dX, dW).
+//
+// gfx950 design:
+//  * 256-thread workgroup (4 waves, 2x2), 128x128 output tile, BK = 64, v_mfma_f32_16x16x32_bf16.
+//  * Operands staged global -> VGPR -> LDS (double-buffered, one barrier per K step); the
+//    next K tile's global loads are issued before the current tile's MFMAs.
+//  * Either operand may be K-contiguous (row fragments via ds_read_b128 from an XOR-swizzled
+//    [rows][64] image) or M/N-contiguous (column fragments via ds_read_b64_tr_b16 from a
+//    swizzled [64][rows] image): forward Y = X W^T, dX = dY W and dW = dY^T X all run without
+//    materialised transposes.
+//  * MFMA operands are swapped (A-slot <- weight/N fragment, B-slot <- activation/M fragment)
+//    so each lane ends with 4 consecutive output columns of one row: 8-byte bf16 stores.
+//  * XCD-aware, grouped tile order: consecutive tiles of one XCD share A/B panels in its L2.
+// Epilogue order mirrors the reference's bf16 module chain (see cullavo_capi.h).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kTileBytes = 128 * 64 * 2;  // 16 KiB per operand tile
+
+typedef __attribute__((ext_vector_type(8))) __bf16 frag8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct GemmArgs {
+  const u16* A;
+  const u16* B;
+  void* C;
+  const u16* bias;
+  u16* preact;
+  const u16* residual;
+  int64_t M, N, K, lda, ldb, ldc, ldr;
+  float alpha, beta;
+  int act;
+  int tiles_m, tiles_n;
+};
+
+// ---- LDS images -----------------------------------------------------------------------------
+// layout 0 image: [128 rows][64 k], 16 B chunk c of row r at chunk slot c ^ ((r >> 1) & 7)
+DEV int img0_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// layout 1 image: [64 k][128 rows], 32 B unit u of k-row k at unit slot u ^ swz(k)
+DEV int swz1(int k) { return (k & 7) ^ (((k >> 3) & 1) << 2); }
+DEV int img1_off(int k, int unit) { return k * 256 + ((unit ^ swz1(k)) << 5); }
+
+// global -> registers for one 128 x 64 operand tile (4 x 16 B per thread)
+template <int LAYOUT>
+DEV void load_tile(const u16* __restrict__ X, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0,
+                   int64_t K, u16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = t + 256 * i;
+    if (LAYOUT == 0) {
+      const int row = q >> 3, c = q & 7;
+      const int64_t gi = idx0 + row, gk = k0 + c * 8;
+      r[i] = (gi < idx_max && gk < K) ? *reinterpret_cast<const u16x8*>(X + gi * ld + gk) : u16x8(0);
+    } else {
+      const int k = q >> 4, ch = q & 15;
+      const int64_t gk = k0 + k, gi = idx0 + ch * 8;
+      r[i] = (gk < K && gi < idx_max) ? *reinterpret_cast<const u16x8*>(X + gk * ld + gi) : u16x8(0);
+    }
+  }
+}
+
+template <int LAYOUT>
+DEV void store_tile(char* lds, const u16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = t + 256 * i;
+    int off;
+    if (LAYOUT == 0) {
+      off = img0_off(q >> 3, q & 7);
+    } else {
+      const int k = q >> 4, ch = q & 15;
+      off = img1_off(k, ch >> 1) + ((ch & 1) << 4);
+    }
+    *reinterpret_cast<u16x8*>(lds + off) = r[i];
+  }
+}
+
+// fragment X[idx = rbase + (lane&15)][k = ks*32 + 8*(lane>>4) + j], j = 0..7
+template <int LAYOUT>
+DEV frag8 read_frag(const char* lds, int rbase, int ks, int lane) {
+  if (LAYOUT == 0) {
+    const int row = rbase + (lane & 15);
+    const int c = ks * 4 + (lane >> 4);
+    u16x8 v = *reinterpret_cast<const u16x8*>(lds + img0_off(row, c));
+    return __builtin_bit_cast(frag8, v);
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int unit = rbase >> 4;
+    s16x4 lo, hi;
+    {
+      const int k = ks * 32 + 8 * g + q;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1_off(k, unit) + 8 * p));
+    }
+    {
+      const int k = ks * 32 + 8 * g + 4 + q;
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1_off(k, unit) + 8 * p));
+    }
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(frag8, v);
+  }
+}
+
+DEV float act_apply(int act, float x) {
+  if (act == CULLAVO_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  if (act == CULLAVO_ACT_QUICK_GELU) return x / (1.f + __expf(-1.702f * x));
+  return x;
+}
+
+// bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
+DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <int AL, int BL, int CT>
+__global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define sA(i) (smem + 2 * (i) * kTileBytes)
+#define sB(i) (smem + 2 * (i) * kTileBytes + kTileBytes)
+
+  // tile order: XCD-contiguous chunks, then groups of 8 M-tiles sweeping N
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * p.tiles_n;
+  const int group = lid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  const int tm_idx = first_m + (lid % per_group) % gsize;
+  const int tn_idx = (lid % per_group) / gsize;
+  const int64_t m0 = (int64_t)tm_idx * BM, n0 = (int64_t)tn_idx * BN;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)cdiv(p.K, BK);
+  u16x8 ra[4], rb[4];
+  load_tile<AL>(p.A, p.lda, m0, p.M, 0, p.K, ra);
+  load_tile<BL>(p.B, p.ldb, n0, p.N, 0, p.K, rb);
+  store_tile<AL>(sA(0), ra);
+  store_tile<BL>(sB(0), rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_tile<AL>(p.A, p.lda, m0, p.M, (int64_t)(kt + 1) * BK, p.K, ra);
+      load_tile<BL>(p.B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BK, p.K, rb);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      frag8 fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fa[t] = read_frag<AL>(sA(cur), wm * 64 + t * 16, ks, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) fb[t] = read_frag<BL>(sB(cur), wn * 64 + t * 16, ks, lane);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<AL>(sA(cur ^ 1), ra);
+      store_tile<BL>(sB(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n .. n+3] --------------------------------------------------
+#pragma unroll
+  for (int tm = 0; tm < 4; ++tm) {
+    const int64_t m = m0 + wm * 64 + tm * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int64_t n = n0 + wn * 64 + tn * 16 + (lane >> 4) * 4;
+      if (n >= p.N) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[tm][tn][j] * p.alpha;
+      if (p.bias) {
+        const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += bf2f(bv[j]);
+      }
+      if (p.act != CULLAVO_ACT_NONE || p.preact) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);
+        if (p.preact) {
+          u16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+          *reinterpret_cast<u16x4*>(p.preact + m * p.ldc + n) = o;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_apply(p.act, v[j]);
+      }
+      if (p.residual) {
+        const u16x4 rv = *reinterpret_cast<const u16x4*>(p.residual + m * p.ldr + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
+      }
+      if (CT == CULLAVO_DT_BF16) {
+        u16* cp = (u16*)p.C + m * p.ldc + n;
+        if (p.beta != 0.f) {
+          const u16x4 old = *reinterpret_cast<const u16x4*>(cp);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += p.beta * bf2f(old[j]);
+        }
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+        *reinterpret_cast<u16x4*>(cp) = o;
+      } else {
+        float* cp = (float*)p.C + m * p.ldc + n;
+        f32x4 o;
+        if (p.beta != 0.f) {
+          const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = v[j] + p.beta * old[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = v[j];
+        }
+        *reinterpret_cast<f32x4*>(cp) = o;
+      }
+    }
+  }
+}
+
+template <int AL, int BL, int CT>
+int launch(const GemmArgs& p, hipStream_t s) {
+  const int smem = 4 * kTileBytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_k<AL, BL, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  gemm_k<AL, BL, CT><<<p.tiles_m * p.tiles_n, 256, smem, s>>>(p);
+  return cullavo_check_launch("gemm");
+}
+
+}  // namespace
+
+extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K, const void* A,
+                            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
+                            float alpha, const void* bias, int act, void* preact, const void* residual,
+                            int64_t ldr, float beta, void* stream) {
+  CV_REQUIRE(a_layout == 0 || a_layout == 1, CULLAVO_EINVAL, "a_layout");
+  CV_REQUIRE(b_layout == 0 || b_layout == 1, CULLAVO_EINVAL, "b_layout");
+  CV_REQUIRE(M >= 0 && N >= 0 && K >= 0, CULLAVO_EINVAL, "negative size");
+  CV_REQUIRE(K % 8 == 0 && N % 8 == 0, CULLAVO_EINVAL, "K and N must be multiples of 8");
+  CV_REQUIRE(a_layout == 0 || M % 8 == 0, CULLAVO_EINVAL, "M must be a multiple of 8 for a_layout 1");
+  CV_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 && (residual == nullptr || ldr % 8 == 0),
+             CULLAVO_EINVAL, "leading dimensions must be multiples of 8");
+  CV_REQUIRE(lda >= (a_layout == 0 ? K : M) && ldb >= (b_layout == 0 ? K : N) && ldc >= N,
+             CULLAVO_EINVAL, "leading dimension too small");
+  CV_REQUIRE(c_dtype == CULLAVO_DT_BF16 || c_dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "c_dtype");
+  CV_REQUIRE(act >= CULLAVO_ACT_NONE && act <= CULLAVO_ACT_QUICK_GELU, CULLAVO_EINVAL, "act");
+  if (M == 0 || N == 0) return CULLAVO_OK;
+  const int64_t tm = cdiv(M, BM), tn = cdiv(N, BN);
+  CV_REQUIRE(tm * tn < (1ll << 31), CULLAVO_EINVAL, "too many tiles");
+  GemmArgs p;
+  p.A = (const u16*)A; p.B = (const u16*)B; p.C = C;
+  p.bias = (const u16*)bias; p.preact = (u16*)preact; p.residual = (const u16*)residual;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldr = ldr;
+  p.alpha = alpha; p.beta = beta; p.act = act;
+  p.tiles_m = (int)tm; p.tiles_n = (int)tn;
+  hipStream_t s = CV_STREAM(stream);
+  const bool f32 = c_dtype == CULLAVO_DT_F32;
+  if (a_layout == 0 && b_layout == 0) return f32 ? launch<0, 0, CULLAVO_DT_F32>(p, s) : launch<0, 0, CULLAVO_DT_BF16>(p, s);
+  if (a_layout == 0 && b_layout == 1) return f32 ? launch<0, 1, CULLAVO_DT_F32>(p, s) : launch<0, 1, CULLAVO_DT_BF16>(p, s);
+  if (a_layout == 1 && b_layout == 0) return f32 ? launch<1, 0, CULLAVO_DT_F32>(p, s) : launch<1, 0, CULLAVO_DT_BF16>(p, s);
+  return f32 ? launch<1, 1, CULLAVO_DT_F32>(p, s) : launch<1, 1, CULLAVO_DT_BF16>(p, s);
+}

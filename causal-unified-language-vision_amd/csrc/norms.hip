@@ -1,0 +1,386 @@
+// RMSNorm (Llama) and LayerNorm (CLIP) forward/backward for gfx950.
+// HBM-bound: one wave64 per row, 16 B per lane per access, the row held in registers between
+// the statistics pass and the normalise pass (rows up to 8192 columns).
+// Reference arithmetic: tf:llama/modeling_llama.py:53-70 (LlamaRMSNorm: f32 statistics,
+// weight * x_hat.to(bf16)), torch.nn.LayerNorm as used by tf:clip/modeling_clip.py:353-384,642.
+#include "common.h"
+
+namespace {
+
+constexpr int kRowsPerBlock = 4;   // 4 waves, one row each
+constexpr int kBwdBlocks = 256;    // backward grid (weight-grad partials: 1024 wave slots)
+
+// ------------------------------------------------------------------------------------------
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
+                                                     T* __restrict__ y, float* __restrict__ rstd,
+                                                     int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * cols;
+  float v[NCH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
+      load8(xr + col, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)cols + eps);
+  if (lane == 0) rstd[row] = r;
+  T* yr = y + row * cols;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
+      float wv[8], o[8];
+      load8(w + col, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = wv[j] * Elt<T>::rnd(v[c][j] * r);
+      store8(yr + col, o);
+    }
+  }
+}
+
+template <typename T, int NCH, bool WANT_DW, bool HAS_DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const T* __restrict__ w, const float* __restrict__ rstd,
+                                                     T* __restrict__ dx, const T* __restrict__ dres,
+                                                     float* __restrict__ part, int64_t rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int wslot = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  const int nslots = gridDim.x * kRowsPerBlock;
+  float acc[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  float wv[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) load8(w + col, wv[c]);
+  }
+  for (int64_t row = wslot; row < rows; row += nslots) {
+    const float r = rstd[row];
+    float xv[NCH][8], g[NCH][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) {
+        float d[8];
+        load8(x + row * cols + col, xv[c]);
+        load8(dy + row * cols + col, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = xv[c][j] * r;
+          g[c][j] = d[j] * wv[c][j];
+          dot += g[c][j] * xh;
+          if (WANT_DW) acc[c][j] += d[j] * Elt<T>::rnd(xh);
+        }
+      }
+    }
+    dot = wave_sum(dot) / (float)cols;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r * (g[c][j] - xv[c][j] * r * dot);
+        if (HAS_DRES) {
+          float rr[8];
+          load8(dres + row * cols + col, rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rr[j];
+        }
+        store8(dx + row * cols + col, o);
+      }
+    }
+  }
+  if (WANT_DW) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) store8(part + (int64_t)wslot * cols + col, acc[c]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
+                                                       const T* __restrict__ b, T* __restrict__ y,
+                                                       float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, int64_t rows,
+                                                       int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * cols;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
+      load8(xr + col, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    }
+  }
+  const float mean = wave_sum(s) / (float)cols;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[c][j] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / (float)cols + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = r;
+  }
+  T* yr = y + row * cols;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
+      float wv[8], bv[8], o[8];
+      load8(w + col, wv);
+      load8(b + col, bv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * r * wv[j] + bv[j];
+      store8(yr + col, o);
+    }
+  }
+}
+
+template <typename T, int NCH, bool WANT_DW, bool HAS_DRES>
+__global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const T* __restrict__ w,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       T* __restrict__ dx, const T* __restrict__ dres,
+                                                       float* __restrict__ part, int64_t rows,
+                                                       int cols) {
+  const int lane = threadIdx.x & 63;
+  const int wslot = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  const int nslots = gridDim.x * kRowsPerBlock;
+  float accw[NCH][8], accb[NCH][8], wv[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) accw[c][j] = accb[c][j] = 0.f;
+    const int col = c * 512 + lane * 8;
+    if (col < cols) load8(w + col, wv[c]);
+  }
+  for (int64_t row = wslot; row < rows; row += nslots) {
+    const float mu = mean[row], r = rstd[row];
+    float xh[NCH][8], g[NCH][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) {
+        float d[8];
+        load8(x + row * cols + col, xh[c]);
+        load8(dy + row * cols + col, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xh[c][j] - mu) * r;
+          g[c][j] = d[j] * wv[c][j];
+          sg += g[c][j];
+          sgx += g[c][j] * xh[c][j];
+          if (WANT_DW) {
+            accw[c][j] += d[j] * xh[c][j];
+            accb[c][j] += d[j];
+          }
+        }
+      }
+    }
+    sg = wave_sum(sg) / (float)cols;
+    sgx = wave_sum(sgx) / (float)cols;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r * (g[c][j] - sg - xh[c][j] * sgx);
+        if (HAS_DRES) {
+          float rr[8];
+          load8(dres + row * cols + col, rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += rr[j];
+        }
+        store8(dx + row * cols + col, o);
+      }
+    }
+  }
+  if (WANT_DW) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < cols) {
+        store8(part + (int64_t)wslot * cols + col, accw[c]);
+        store8(part + ((int64_t)nslots + wslot) * cols + col, accb[c]);
+      }
+    }
+  }
+}
+
+// partial [nslots, cols] f32 -> out[c] = beta*out[c] + sum_p part[p][c]
+template <typename TO>
+__global__ __launch_bounds__(256) void reduce_partials_k(const float* __restrict__ part, int nslots,
+                                                         int cols, TO* __restrict__ out, float beta) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= cols) return;
+  float s = 0.f;
+  for (int p = 0; p < nslots; ++p) s += part[(int64_t)p * cols + col];
+  if (beta != 0.f) s += beta * Elt<TO>::ld(out, col);
+  Elt<TO>::st(out, col, s);
+}
+
+int nch_for(int64_t cols) {
+  if (cols <= 512) return 1;
+  if (cols <= 1024) return 2;
+  if (cols <= 2048) return 4;
+  if (cols <= 4096) return 8;
+  return 16;
+}
+
+#define NCH_DISPATCH(nch, ...)               \
+  switch (nch) {                             \
+    case 1: { constexpr int NC = 1; __VA_ARGS__; break; } \
+    case 2: { constexpr int NC = 2; __VA_ARGS__; break; } \
+    case 4: { constexpr int NC = 4; __VA_ARGS__; break; } \
+    case 8: { constexpr int NC = 8; __VA_ARGS__; break; } \
+    default: { constexpr int NC = 16; __VA_ARGS__; break; } \
+  }
+
+template <typename TO>
+void launch_reduce(const float* part, int nslots, int cols, void* out, float beta, hipStream_t s) {
+  reduce_partials_k<TO><<<cdiv(cols, 256), 256, 0, s>>>(part, nslots, cols, (TO*)out, beta);
+}
+
+int bwd_blocks(int64_t rows) { return (int)std::min<int64_t>(kBwdBlocks, cdiv(rows, kRowsPerBlock)); }
+
+}  // namespace
+
+extern "C" size_t cullavo_norm_bwd_workspace(int64_t rows, int64_t cols) {
+  return (size_t)2 * kBwdBlocks * kRowsPerBlock * cols * sizeof(float);
+}
+
+extern "C" int cullavo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows,
+                                   int64_t cols, float eps, int dtype, void* stream) {
+  CV_REQUIRE(cols % 8 == 0 && cols > 0 && cols <= 8192, CULLAVO_EINVAL, "cols must be a multiple of 8 in [8, 8192]");
+  CV_REQUIRE(rows >= 0, CULLAVO_EINVAL, "rows < 0");
+  if (rows == 0) return CULLAVO_OK;
+  const int nb = (int)cdiv(rows, kRowsPerBlock);
+  hipStream_t s = CV_STREAM(stream);
+  const int nch = nch_for(cols);
+  if (dtype == CULLAVO_DT_BF16) {
+    NCH_DISPATCH(nch, rmsnorm_fwd_k<u16, NC><<<nb, 256, 0, s>>>((const u16*)x, (const u16*)w, (u16*)y, rstd, rows, (int)cols, eps));
+  } else if (dtype == CULLAVO_DT_F32) {
+    NCH_DISPATCH(nch, rmsnorm_fwd_k<float, NC><<<nb, 256, 0, s>>>((const float*)x, (const float*)w, (float*)y, rstd, rows, (int)cols, eps));
+  } else {
+    CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  }
+  return cullavo_check_launch("rmsnorm_fwd");
+}
+
+extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
+                                   void* dx, const void* dres, void* dw, int w_dtype, float beta, float* ws,
+                                   int64_t rows, int64_t cols, int dtype, void* stream) {
+  CV_REQUIRE(cols % 8 == 0 && cols > 0 && cols <= 8192, CULLAVO_EINVAL, "cols must be a multiple of 8 in [8, 8192]");
+  CV_REQUIRE(dw == nullptr || ws != nullptr, CULLAVO_EINVAL, "dw requires a workspace");
+  if (rows == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int nb = bwd_blocks(rows);
+  const int nch = nch_for(cols);
+  const bool want = dw != nullptr, hr = dres != nullptr;
+#define RMB(T, WD, HR) NCH_DISPATCH(nch, rmsnorm_bwd_k<T, NC, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols))
+  if (dtype == CULLAVO_DT_BF16) {
+    if (want && hr) { RMB(u16, true, true); } else if (want) { RMB(u16, true, false); }
+    else if (hr) { RMB(u16, false, true); } else { RMB(u16, false, false); }
+  } else if (dtype == CULLAVO_DT_F32) {
+    if (want && hr) { RMB(float, true, true); } else if (want) { RMB(float, true, false); }
+    else if (hr) { RMB(float, false, true); } else { RMB(float, false, false); }
+  } else {
+    CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  }
+#undef RMB
+  if (want) {
+    const int nslots = nb * kRowsPerBlock;
+    if (w_dtype == CULLAVO_DT_BF16) launch_reduce<u16>(ws, nslots, (int)cols, dw, beta, s);
+    else launch_reduce<float>(ws, nslots, (int)cols, dw, beta, s);
+  }
+  return cullavo_check_launch("rmsnorm_bwd");
+}
+
+extern "C" int cullavo_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
+                                     float* rstd, int64_t rows, int64_t cols, float eps, int dtype,
+                                     void* stream) {
+  CV_REQUIRE(cols % 8 == 0 && cols > 0 && cols <= 8192, CULLAVO_EINVAL, "cols must be a multiple of 8 in [8, 8192]");
+  if (rows == 0) return CULLAVO_OK;
+  const int nb = (int)cdiv(rows, kRowsPerBlock);
+  hipStream_t s = CV_STREAM(stream);
+  const int nch = nch_for(cols);
+  if (dtype == CULLAVO_DT_BF16) {
+    NCH_DISPATCH(nch, layernorm_fwd_k<u16, NC><<<nb, 256, 0, s>>>((const u16*)x, (const u16*)w, (const u16*)b, (u16*)y, mean, rstd, rows, (int)cols, eps));
+  } else if (dtype == CULLAVO_DT_F32) {
+    NCH_DISPATCH(nch, layernorm_fwd_k<float, NC><<<nb, 256, 0, s>>>((const float*)x, (const float*)w, (const float*)b, (float*)y, mean, rstd, rows, (int)cols, eps));
+  } else {
+    CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  }
+  return cullavo_check_launch("layernorm_fwd");
+}
+
+extern "C" int cullavo_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
+                                     const float* rstd, void* dx, const void* dres, void* dw, void* db,
+                                     int w_dtype, float beta, float* ws, int64_t rows, int64_t cols,
+                                     int dtype, void* stream) {
+  CV_REQUIRE(cols % 8 == 0 && cols > 0 && cols <= 8192, CULLAVO_EINVAL, "cols must be a multiple of 8 in [8, 8192]");
+  CV_REQUIRE((dw == nullptr) == (db == nullptr), CULLAVO_EINVAL, "dw and db must both be given or both be null");
+  CV_REQUIRE(dw == nullptr || ws != nullptr, CULLAVO_EINVAL, "dw requires a workspace");
+  if (rows == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int nb = bwd_blocks(rows);
+  const int nch = nch_for(cols);
+  const bool want = dw != nullptr, hr = dres != nullptr;
+#define LNB(T, WD, HR) NCH_DISPATCH(nch, layernorm_bwd_k<T, NC, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols))
+  if (dtype == CULLAVO_DT_BF16) {
+    if (want && hr) { LNB(u16, true, true); } else if (want) { LNB(u16, true, false); }
+    else if (hr) { LNB(u16, false, true); } else { LNB(u16, false, false); }
+  } else if (dtype == CULLAVO_DT_F32) {
+    if (want && hr) { LNB(float, true, true); } else if (want) { LNB(float, true, false); }
+    else if (hr) { LNB(float, false, true); } else { LNB(float, false, false); }
+  } else {
+    CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  }
+#undef LNB
+  if (want) {
+    const int nslots = nb * kRowsPerBlock;
+    if (w_dtype == CULLAVO_DT_BF16) {
+      launch_reduce<u16>(ws, nslots, (int)cols, dw, beta, s);
+      launch_reduce<u16>(ws + (int64_t)nslots * cols, nslots, (int)cols, db, beta, s);
+    } else {
+      launch_reduce<float>(ws, nslots, (int)cols, dw, beta, s);
+      launch_reduce<float>(ws + (int64_t)nslots * cols, nslots, (int)cols, db, beta, s);
+    }
+  }
+  return cullavo_check_launch("layernorm_bwd");
+}

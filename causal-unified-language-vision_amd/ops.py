@@ -1,0 +1,324 @@
+"""Torch-facing wrappers of the C-ABI kernels (one function per cullavo_* entry point).
+
+PyTorch owns every tensor (caching allocator); these wrappers only validate shapes, allocate
+outputs/workspaces with torch and pass raw device pointers plus the current HIP stream across
+the boundary (SURVEY.md §8(b) "Ownership", "Threading / streams"). Nothing here computes on
+the CPU: every function requires CUDA(HIP) tensors and fails loudly otherwise.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, DT_BF16, DT_F32, call, lib
+
+__all__ = [
+    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "linear", "linear_dx", "linear_dw",
+    "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "swiglu_fwd", "swiglu_bwd",
+    "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
+    "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
+    "ce_reduce", "ce_bwd", "adamw", "sumsq", "clip_coef", "scale_inplace",
+]
+
+_DT = {torch.bfloat16: DT_BF16, torch.float32: DT_F32}
+
+
+def _dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype} (bf16 / f32 only)") from None
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("cullavo kernels run on the GPU only: got a CPU tensor (no CPU fallback)")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld(t: torch.Tensor) -> int:
+    """leading dimension (row stride, elements) of a 2-D row-major view"""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D view with unit column stride")
+    return t.stride(0)
+
+
+# ---- GEMM ------------------------------------------------------------------------------------
+def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
+         alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
+         beta: float = 0.0):
+    _dev(A, B, C, bias, preact, residual)
+    call("gemm", a_layout, b_layout, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _dt(C), float(alpha),
+         _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _stream())
+    return C
+
+
+def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: bool = False, out=None):
+    """y = act(x @ w.T + bias) (+ residual); x [M,K] (row stride may exceed K), w [N,K]."""
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"linear: x {tuple(x.shape)} vs w {tuple(w.shape)}")
+    y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
+    pre = torch.empty((M, N), dtype=x.dtype, device=x.device) if want_preact else None
+    gemm(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
+         residual=residual, ldr=_ld(residual) if residual is not None else 0)
+    return (y, pre) if want_preact else y
+
+
+def linear_dx(dy, w, *, residual=None, out=None):
+    """dx = dy @ w (+ residual); dy [M,N], w [N,K] -> [M,K]"""
+    M, N = dy.shape
+    K = w.shape[1]
+    dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
+    gemm(0, 1, M, K, N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), residual=residual,
+         ldr=_ld(residual) if residual is not None else 0)
+    return dx
+
+
+def linear_dw(dy, x, out, *, beta: float = 0.0):
+    """out[N,K] = dy^T x (+ beta*out); dy [M,N], x [M,K]"""
+    M, N = dy.shape
+    K = x.shape[1]
+    if out.shape != (N, K):
+        raise ValueError(f"linear_dw: out {tuple(out.shape)} != {(N, K)}")
+    gemm(1, 1, N, K, M, dy, _ld(dy), x, _ld(x), out, _ld(out), beta=beta)
+    return out
+
+
+# ---- norms -----------------------------------------------------------------------------------
+def rmsnorm_fwd(x, w, eps: float):
+    _dev(x, w)
+    rows, cols = x.shape
+    y = torch.empty_like(x)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    call("rmsnorm_fwd", _ptr(x), _ptr(w), _ptr(y), _ptr(rstd), rows, cols, float(eps), _dt(x), _stream())
+    return y, rstd
+
+
+def _norm_ws(rows, cols, device):
+    n = lib().cullavo_norm_bwd_workspace(rows, cols) // 4
+    return torch.empty(n, dtype=torch.float32, device=device)
+
+
+def rmsnorm_bwd(dy, x, w, rstd, *, dres=None, dw=None, beta: float = 0.0):
+    _dev(dy, x, w, rstd, dres, dw)
+    rows, cols = x.shape
+    dx = torch.empty_like(x)
+    ws = _norm_ws(rows, cols, x.device) if dw is not None else None
+    call("rmsnorm_bwd", _ptr(dy), _ptr(x), _ptr(w), _ptr(rstd), _ptr(dx), _ptr(dres), _ptr(dw),
+         _dt(dw) if dw is not None else DT_BF16, float(beta), _ptr(ws), rows, cols, _dt(x), _stream())
+    return dx
+
+
+def layernorm_fwd(x, w, b, eps: float):
+    _dev(x, w, b)
+    rows, cols = x.shape
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    call("layernorm_fwd", _ptr(x), _ptr(w), _ptr(b), _ptr(y), _ptr(mean), _ptr(rstd), rows, cols, float(eps),
+         _dt(x), _stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, *, dres=None, dw=None, db=None, beta: float = 0.0):
+    _dev(dy, x, w, mean, rstd, dres, dw, db)
+    rows, cols = x.shape
+    dx = torch.empty_like(x)
+    ws = _norm_ws(rows, cols, x.device) if dw is not None else None
+    call("layernorm_bwd", _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx), _ptr(dres), _ptr(dw),
+         _ptr(db), _dt(dw) if dw is not None else DT_BF16, float(beta), _ptr(ws), rows, cols, _dt(x), _stream())
+    return dx
+
+
+# ---- element-wise ----------------------------------------------------------------------------
+def swiglu_fwd(gu):
+    _dev(gu)
+    rows, F2 = gu.shape
+    out = torch.empty((rows, F2 // 2), dtype=gu.dtype, device=gu.device)
+    call("swiglu_fwd", _ptr(gu), rows, F2 // 2, _ptr(out), _dt(gu), _stream())
+    return out
+
+
+def swiglu_bwd(dout, gu):
+    _dev(dout, gu)
+    rows, F2 = gu.shape
+    dgu = torch.empty_like(gu)
+    call("swiglu_bwd", _ptr(dout), _ptr(gu), rows, F2 // 2, _ptr(dgu), _dt(gu), _stream())
+    return dgu
+
+
+def act_bwd(act: int, dy, preact):
+    _dev(dy, preact)
+    dx = torch.empty_like(dy)
+    call("act_bwd", act, _ptr(dy), _ptr(preact), _ptr(dx), dy.numel(), _dt(dy), _stream())
+    return dx
+
+
+def colsum(x, out, *, beta: float = 0.0):
+    _dev(x, out)
+    rows, cols = x.shape
+    ws = torch.empty(lib().cullavo_colsum_workspace(rows, cols) // 4, dtype=torch.float32, device=x.device)
+    call("colsum", _ptr(x), rows, cols, _ptr(out), _dt(out), float(beta), _ptr(ws), _dt(x), _stream())
+    return out
+
+
+def rope(q, k, position_ids, *, hq: int, hk: int, head_dim: int, theta: float, inverse: bool = False):
+    """in-place rotary embedding of q [T, >=hq*D] and k [T, >=hk*D] (views with row strides)"""
+    _dev(q, k, position_ids)
+    T = q.shape[0]
+    call("rope", _ptr(q), _ld(q), _ptr(k), _ld(k) if k is not None else 0, _ptr(position_ids), T, hq, hk,
+         head_dim, float(theta), int(inverse), _dt(q), _stream())
+
+
+# ---- attention -------------------------------------------------------------------------------
+def attn_fwd(q, k, v, *, B: int, H: int, Lq: int, Lk: int, D: int, scale: float, causal: bool,
+             kv_start=None, out=None):
+    """q/k/v: [B*L, >=H*D] row-strided views. Returns (o [B*Lq, H*D], lse [B,H,Lq] f32)."""
+    _dev(q, k, v, kv_start)
+    o = out if out is not None else torch.empty((B * Lq, H * D), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B, H, Lq), dtype=torch.float32, device=q.device)
+    call("attn_fwd", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(o), _ld(o), _ptr(lse), B, H, Lq, Lk,
+         D, float(scale), int(causal), _ptr(kv_start), _dt(q), _stream())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, *, B: int, H: int, Lq: int, Lk: int, D: int, scale: float, causal: bool,
+             kv_start=None, dq=None, dk=None, dv=None):
+    _dev(q, k, v, o, do, lse, kv_start)
+    dq = dq if dq is not None else torch.empty((B * Lq, H * D), dtype=q.dtype, device=q.device)
+    dk = dk if dk is not None else torch.empty((B * Lk, H * D), dtype=q.dtype, device=q.device)
+    dv = dv if dv is not None else torch.empty((B * Lk, H * D), dtype=q.dtype, device=q.device)
+    delta = torch.empty((B, H, Lq), dtype=torch.float32, device=q.device)
+    call("attn_bwd", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(o), _ld(o), _ptr(do), _ld(do),
+         _ptr(lse), _ptr(delta), _ptr(dq), _ld(dq), _ptr(dk), _ld(dk), _ptr(dv), _ld(dv), B, H, Lq, Lk, D,
+         float(scale), int(causal), _ptr(kv_start), _dt(q), _stream())
+    return dq, dk, dv
+
+
+# ---- embeddings / merge ----------------------------------------------------------------------
+def embedding_fwd(ids, table):
+    _dev(ids, table)
+    ids = ids.reshape(-1)
+    vocab, dim = table.shape
+    out = torch.empty((ids.numel(), dim), dtype=table.dtype, device=table.device)
+    call("embedding_fwd", _ptr(ids), ids.numel(), _ptr(table), vocab, dim, _ptr(out), _dt(table), _stream())
+    return out
+
+
+def embedding_bwd(ids, dout, dtable, *, beta: float = 0.0):
+    _dev(ids, dout, dtable)
+    ids = ids.reshape(-1)
+    vocab, dim = dtable.shape
+    call("embedding_bwd", _ptr(ids), ids.numel(), _ptr(dout), vocab, dim, _ptr(dtable), _dt(dtable), float(beta),
+         _dt(dout), _stream())
+    return dtable
+
+
+def im2col_patches(pixels, patch: int, kpad: int):
+    _dev(pixels)
+    B, C, H, W = pixels.shape
+    P = (H // patch) * (W // patch)
+    out = torch.empty((B * (1 + P), kpad), dtype=torch.bfloat16, device=pixels.device)
+    pixels = pixels.contiguous()
+    call("im2col_patches", _ptr(pixels), _dt(pixels), B, C, H, W, patch, _ptr(out), kpad, _stream())
+    return out
+
+
+def vision_embed_ln(x, cls, pos, w, b, *, B: int, T: int, eps: float):
+    _dev(x, cls, pos, w, b)
+    y = torch.empty_like(x)
+    call("vision_embed_ln", _ptr(x), _ptr(cls), _ptr(pos), _ptr(w), _ptr(b), _ptr(y), B, T, x.shape[1],
+         float(eps), _stream())
+    return y
+
+
+def merge_plan(ids, mask, *, L: int, image_token: int, n_patches: int, left_padding: bool):
+    _dev(ids, mask)
+    B, S = ids.shape
+    dev = ids.device
+    text_dst = torch.empty((B, S), dtype=torch.int64, device=dev)
+    src = torch.empty((B, L), dtype=torch.int64, device=dev)
+    mmask = torch.empty((B, L), dtype=torch.int64, device=dev)
+    pos = torch.empty((B, L), dtype=torch.int64, device=dev)
+    ids = ids.contiguous()
+    mask = mask.contiguous().to(torch.int64) if mask is not None else None
+    call("merge_plan", _ptr(ids), _ptr(mask), B, S, L, int(image_token), int(n_patches), int(left_padding),
+         _ptr(text_dst), _ptr(src), _ptr(mmask), _ptr(pos), _stream())
+    return text_dst, src, mmask, pos
+
+
+def row_gather2(src, a, b):
+    _dev(src, a, b)
+    dim = a.shape[-1]
+    a2 = a.reshape(-1, dim)
+    b2 = b.reshape(-1, dim) if b is not None else a2
+    out = torch.empty((src.numel(), dim), dtype=a.dtype, device=a.device)
+    call("row_gather2", _ptr(src), src.numel(), _ptr(a2), a2.shape[0], _ptr(b2), dim, _ptr(out), _dt(a), _stream())
+    return out
+
+
+# ---- loss ------------------------------------------------------------------------------------
+def shift_targets(labels, mask, ignore_index: int = -100):
+    _dev(labels, mask)
+    B, L = labels.shape
+    tgt = torch.empty((B * L,), dtype=torch.int64, device=labels.device)
+    labels = labels.contiguous().to(torch.int64)
+    mask = mask.contiguous().to(torch.int64) if mask is not None else None
+    call("shift_targets", _ptr(labels), _ptr(mask), B, L, int(ignore_index), _ptr(tgt), _stream())
+    return tgt
+
+
+def ce_fwd(logits, targets, ignore_index: int = -100):
+    _dev(logits, targets)
+    rows, V = logits.shape
+    row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    call("ce_fwd", _ptr(logits), _ld(logits), _ptr(targets), rows, V, int(ignore_index), _ptr(row_loss),
+         _ptr(row_lse), _dt(logits), _stream())
+    return row_loss, row_lse
+
+
+def ce_reduce(row_loss, targets, ignore_index: int = -100):
+    out = torch.empty(3, dtype=torch.float32, device=row_loss.device)
+    call("ce_reduce", _ptr(row_loss), _ptr(targets), row_loss.numel(), int(ignore_index), _ptr(out), _stream())
+    return out
+
+
+def ce_bwd(logits, targets, row_lse, loss_out, grad_loss=None, ignore_index: int = -100, out=None):
+    _dev(logits, targets, row_lse, loss_out, grad_loss)
+    rows, V = logits.shape
+    d = out if out is not None else torch.empty_like(logits)
+    call("ce_bwd", _ptr(logits), _ld(logits), _ptr(targets), _ptr(row_lse), _ptr(loss_out), _ptr(grad_loss), rows,
+         V, int(ignore_index), _ptr(d), _ld(d), _dt(logits), _stream())
+    return d
+
+
+# ---- optimiser -------------------------------------------------------------------------------
+def adamw(param, grad, exp_avg, exp_avg_sq, *, lr: float, beta1: float, beta2: float, eps: float,
+          weight_decay: float, step: int, grad_scale=None):
+    _dev(param, grad, exp_avg, exp_avg_sq, grad_scale)
+    call("adamw", _ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), param.numel(), float(lr),
+         float(beta1), float(beta2), float(eps), float(weight_decay), int(step), _ptr(grad_scale), _dt(param),
+         _dt(exp_avg), _stream())
+
+
+def sumsq(x, out):
+    _dev(x, out)
+    call("sumsq", _ptr(x), x.numel(), _ptr(out), _dt(x), _stream())
+
+
+def clip_coef(sumsq_buf, max_norm: float, coef, norm_out=None):
+    call("clip_coef", _ptr(sumsq_buf), float(max_norm), _ptr(coef), _ptr(norm_out), _stream())
+
+
+def scale_inplace(x, scale):
+    call("scale_inplace", _ptr(x), x.numel(), _ptr(scale), _dt(x), _stream())

@@ -1,0 +1,196 @@
+/*
+ * cullavo_capi.h — the C-ABI of libcullavo_hip.so, the MI355X (gfx950) kernels behind the
+ * CuLLaVO forward/backward hot path.
+ *
+ * Boundary rules:
+ *   - plain pointers, sizes and scalars only; no torch / HIP types in the signatures;
+ *   - every function is stream-ordered on the `stream` argument (a hipStream_t passed as void*,
+ *     normally torch.cuda.current_stream().cuda_stream) and never allocates, frees or syncs:
+ *     scratch is passed in by the caller (sizes from the *_workspace() helpers);
+ *   - every function returns 0 on success or a CULLAVO_E* code; cullavo_last_error() returns
+ *     the message of the last failure on the calling thread. The Python wrappers raise
+ *     RuntimeError / ValueError from these, mirroring the reference's ValueError for a bad
+ *     feature-select strategy (reference cullavo/arch_cullavo.py:595-597).
+ *
+ * Each entry point names the reference computation it replaces (reference = the
+ * LTTTDH/Causal-Unified-Language-Vision tree; "tf:" = the HuggingFace transformers modules the
+ * reference reaches through cullavo/arch_cullavo.py:582-665).
+ * Layout conventions: activations are row-major [rows, cols] with a leading dimension in
+ * elements; "tokens" = batch * sequence rows.
+ */
+#ifndef CULLAVO_CAPI_H
+#define CULLAVO_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- dtypes / codes ------------------------------------------------------------------- */
+#define CULLAVO_DT_F32 0
+#define CULLAVO_DT_BF16 1
+
+#define CULLAVO_OK 0
+#define CULLAVO_EINVAL 1       /* bad shape / argument */
+#define CULLAVO_EUNSUPPORTED 2 /* dtype or shape the kernels do not implement */
+#define CULLAVO_EHIP 3         /* a HIP runtime error (launch failure) */
+
+/* activation codes used by the GEMM epilogue and cullavo_act_bwd */
+#define CULLAVO_ACT_NONE 0
+#define CULLAVO_ACT_GELU 1       /* erf GELU: LlavaMultiModalProjector act (tf:llava/modeling_llava.py:99) */
+#define CULLAVO_ACT_QUICK_GELU 2 /* x*sigmoid(1.702x): CLIPMLP act (tf:activations.py:117-123) */
+
+int cullavo_abi_version(void);
+const char* cullavo_last_error(void);
+
+/* ---- GEMM (MFMA bf16, fp32 accumulate) --------------------------------------------------
+ * C[M,N] = alpha * sum_k A(m,k) B(k,n)  [+ bias[n]] -> [preact] -> act -> [+ residual] [+ beta*C]
+ * a_layout 0: A stored [M,K] (K contiguous, lda >= K)      -- activations
+ * a_layout 1: A stored [K,M] (M contiguous, lda >= M)      -- dW = dY^T X
+ * b_layout 0: B stored [N,K] (K contiguous, nn.Linear.weight)
+ * b_layout 1: B stored [K,N] (N contiguous)                -- dX = dY W
+ * Replaces every nn.Linear of CLIP / projector / Llama (tf:clip/modeling_clip.py:280-351,
+ * tf:llava/modeling_llava.py:87-107, tf:llama/modeling_llama.py:163-282, lm_head :480) and their
+ * autograd backward. A,B,residual,bias,preact are bf16; C is bf16 or f32 (c_dtype).
+ * Rounding follows the reference's bf16 module chain: pre = bf16(acc+bias); out = bf16(act(pre));
+ * with a residual: out = bf16(out + residual). beta accumulates into C: C = out + beta*C
+ * (gradient accumulation into the parameter-gradient arena). */
+int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
+                 const void* A, int64_t lda, const void* B, int64_t ldb,
+                 void* C, int64_t ldc, int c_dtype, float alpha,
+                 const void* bias, int act, void* preact,
+                 const void* residual, int64_t ldr, float beta, void* stream);
+
+/* ---- norms -------------------------------------------------------------------------------
+ * LlamaRMSNorm (tf:llama/modeling_llama.py:53-70): fp32 statistics, y = w * bf16(x*rstd).
+ * rstd: [rows] f32 saved for backward. cols % 8 == 0, cols <= 8192. */
+int cullavo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int64_t rows,
+                        int64_t cols, float eps, int dtype, void* stream);
+/* dx (dtype) and optionally dw (w_dtype, nullable; beta accumulates into dw) */
+int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                        const void* dres, void* dw, int w_dtype, float beta, float* workspace,
+                        int64_t rows, int64_t cols, int dtype, void* stream);
+/* nn.LayerNorm (CLIP pre_layrnorm / layer_norm1/2, tf:clip/modeling_clip.py:353-384,642).
+ * mean/rstd: [rows] f32 saved for backward. The backwards add an optional residual-stream
+ * gradient dres (nullable) into dx, fusing the residual branch join. */
+int cullavo_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean,
+                          float* rstd, int64_t rows, int64_t cols, float eps, int dtype,
+                          void* stream);
+int cullavo_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean,
+                          const float* rstd, void* dx, const void* dres, void* dw, void* db,
+                          int w_dtype, float beta, float* workspace, int64_t rows, int64_t cols,
+                          int dtype, void* stream);
+/* bytes of f32 workspace the norm backward needs for the weight-gradient partials */
+size_t cullavo_norm_bwd_workspace(int64_t rows, int64_t cols);
+
+/* ---- element-wise ------------------------------------------------------------------------ */
+/* LlamaMLP act: out = silu(gate) * up  (tf:llama/modeling_llama.py:163-176). gu is the fused
+ * gate|up projection output [rows, 2F] (gate in columns [0,F), up in [F,2F)); out [rows, F].
+ * The backward writes dgu [rows, 2F] in the same fused layout. */
+int cullavo_swiglu_fwd(const void* gu, int64_t rows, int64_t F, void* out, int dtype,
+                       void* stream);
+int cullavo_swiglu_bwd(const void* dout, const void* gu, int64_t rows, int64_t F, void* dgu,
+                       int dtype, void* stream);
+/* dx = dy * act'(preact) for CULLAVO_ACT_GELU / CULLAVO_ACT_QUICK_GELU */
+int cullavo_act_bwd(int act, const void* dy, const void* preact, void* dx, int64_t n, int dtype,
+                    void* stream);
+/* out[c] = beta*out[c] + sum_r x[r,c] (bias gradients); out dtype = out_dtype */
+int cullavo_colsum(const void* x, int64_t rows, int64_t cols, void* out, int out_dtype,
+                   float beta, float* workspace, int dtype, void* stream);
+size_t cullavo_colsum_workspace(int64_t rows, int64_t cols);
+/* Llama rotary embedding, rotate_half form (tf:llama/modeling_llama.py:73-160), in place on
+ * q [tokens, hq*D] and k [tokens, hk*D] (row strides ldq, ldk). inv_freq = theta^(-2i/D);
+ * cos/sin of pos*inv_freq are computed in f32 and rounded to bf16 as the reference does.
+ * inverse=1 applies the transpose rotation (the backward). */
+int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const int64_t* position_ids,
+                 int64_t tokens, int hq, int hk, int head_dim, float theta, int inverse,
+                 int dtype, void* stream);
+
+/* ---- attention (flash-style, MFMA bf16) --------------------------------------------------
+ * Replaces tf:llama/modeling_llama.py:191-282 (causal, D=128, FA2 in the reference,
+ * cullavo/load_cullavo.py:72) and tf:clip/modeling_clip.py:280-336 (non-causal, D=64).
+ * q,k,v,o: [B, L, H, D] with token stride ld* elements (head h at column h*D).
+ * lse: [B, H, Lq] f32 natural-log log-sum-exp of the scaled scores (saved for backward).
+ * kv_start: nullable int32 [B]: keys < kv_start[b] are masked (left padding).
+ * D in {64, 128}; Lq == Lk when causal. */
+int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                     int64_t ldv, void* o, int64_t ldo, float* lse, int B, int H, int Lq, int Lk,
+                     int D, float scale, int causal, const int32_t* kv_start, int dtype,
+                     void* stream);
+/* delta workspace: [B, H, Lq] f32 (= rowsum(dO*O)); dq,dk,dv same layout as q,k,v */
+int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                     int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                     const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
+                     int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
+                     float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
+
+/* ---- embeddings / merge ------------------------------------------------------------------ */
+/* get_input_embeddings()(input_ids) (reference cullavo/arch_cullavo.py:582) */
+int cullavo_embedding_fwd(const int64_t* ids, int64_t n, const void* table, int64_t vocab,
+                          int64_t dim, void* out, int dtype, void* stream);
+/* dtable[v] = beta*dtable[v] + sum_{i: ids[i]==v} dout[i] for every v that occurs in ids;
+ * rows that do not occur are left untouched (caller zeroes for beta=0). Deterministic. */
+int cullavo_embedding_bwd(const int64_t* ids, int64_t n, const void* dout, int64_t vocab,
+                          int64_t dim, void* dtable, int table_dtype, float beta, int dtype,
+                          void* stream);
+/* CLIP patch embedding front end (tf:clip/modeling_clip.py:202-218): pixels [B,3,H,W] (f32 or
+ * bf16 by pix_dtype) -> patches [B*(1+P), kpad] bf16, row b*(1+P) (the CLS slot) all zeros,
+ * column order (c, i, j) like Conv2d.weight.reshape(out, -1), zero pad to kpad. */
+int cullavo_im2col_patches(const void* pixels, int pix_dtype, int B, int C, int H, int W,
+                           int patch, void* out, int64_t kpad, void* stream);
+/* x[b,t] += (t==0 ? cls : 0) + pos[t] then LayerNorm (pre_layrnorm); x: [B*T, dim] bf16 */
+int cullavo_vision_embed_ln(const void* x, const void* cls, const void* pos, const void* w,
+                            const void* b, void* y, int B, int T, int64_t dim, float eps,
+                            void* stream);
+/* The llava _merge_input_ids_with_image_features index plan (transformers ~4.37, called at
+ * reference cullavo/arch_cullavo.py:600-602). ids/mask: [B,S]; per text token its merged
+ * row (text_dst [B,S], -1 for image tokens), per merged row its source (src [B,L]: text row
+ * b*S+s, or B*S + image row, or -1 for zero fill), merged mask [B,L] and position_ids [B,L].
+ * n_patches = image feature rows per image. Returns CULLAVO_EINVAL when the image-token count
+ * does not match n_images (the reference's ValueError). img_count/left_pad from host. */
+int cullavo_merge_plan(const int64_t* ids, const int64_t* mask, int B, int S, int L,
+                       int64_t image_token, int64_t n_patches, int left_padding,
+                       int64_t* text_dst, int64_t* src, int64_t* merged_mask,
+                       int64_t* position_ids, void* stream);
+/* out[r] = src[r] < 0 ? 0 : (src[r] < n_a ? a[src[r]] : b[src[r]-n_a]), rows of dim */
+int cullavo_row_gather2(const int64_t* src, int64_t rows, const void* a, int64_t n_a,
+                        const void* b, int64_t dim, void* out, int dtype, void* stream);
+
+/* ---- loss ---------------------------------------------------------------------------------
+ * Shifted, attention-masked CE (reference cullavo/arch_cullavo.py:651-665): target for row
+ * (b,t) is labels[b,t+1] when t+1 < L and mask[b,t+1] != 0, else -100 (ignored). */
+int cullavo_shift_targets(const int64_t* labels, const int64_t* mask, int B, int L,
+                          int64_t ignore_index, int64_t* targets, void* stream);
+/* per-row loss (0 for ignored rows) and lse; logits [rows, V] bf16 with row stride ldl */
+int cullavo_ce_fwd(const void* logits, int64_t ldl, const int64_t* targets, int64_t rows,
+                   int64_t V, int64_t ignore_index, float* row_loss, float* row_lse, int dtype,
+                   void* stream);
+/* loss_out[0] = sum(row_loss)/count, loss_out[1] = count, loss_out[2] = 1/count */
+int cullavo_ce_reduce(const float* row_loss, const int64_t* targets, int64_t rows,
+                      int64_t ignore_index, float* loss_out, void* stream);
+/* dlogits = (softmax - onehot) * grad_loss[0] * loss_out[2] for non-ignored rows, 0 otherwise */
+int cullavo_ce_bwd(const void* logits, int64_t ldl, const int64_t* targets, const float* row_lse,
+                   const float* loss_out, const float* grad_loss, int64_t rows, int64_t V,
+                   int64_t ignore_index, void* dlogits, int64_t ldd, int dtype, void* stream);
+
+/* ---- optimiser -----------------------------------------------------------------------------
+ * torch.optim.AdamW semantics (reference trainer/cullavo_trainer.py:12-14) with an optional
+ * device-side gradient scale (the clip_grad_norm_ coefficient, reference
+ * pipeline/CuLLaVOPipeline.py:90-91). States have state_dtype, params/grads dtype. */
+int cullavo_adamw(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
+                  float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
+                  const float* grad_scale, int dtype, int state_dtype, void* stream);
+/* out[0] += sum(grad^2) (f32, device); run over every grad buffer, then cullavo_clip_coef */
+int cullavo_sumsq(const void* x, int64_t n, float* out, int dtype, void* stream);
+/* coef[0] = min(1, max_norm / (sqrt(sumsq[0]) + 1e-6)); norm_out[0] = sqrt(sumsq[0]) */
+int cullavo_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out,
+                      void* stream);
+/* y = x * scale[0] in place (n elements) */
+int cullavo_scale_inplace(void* x, int64_t n, const float* scale, int dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CULLAVO_CAPI_H */
