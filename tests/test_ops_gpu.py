@@ -1,0 +1,371 @@
+"""Per-kernel parity: every C-ABI kernel on the MI355X against the CPU oracle / an fp32 torch
+restatement of the same op on the same (bf16-rounded) inputs.
+
+Tolerances (stated per test): bf16 storage has a relative step of 2^-8 = 3.9e-3, so kernels
+whose output is bf16 are checked at max|err| <= c * 2^-8 * scale with c small, and integer /
+index work (merge plan, targets, gathers, embedding rows) bit-exactly.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import cullavo_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def ops():
+    from cullavo_amd import ops as _ops
+    return _ops
+
+
+def rnd(shape, seed, scale=1.0, dtype=BF):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(dtype)
+
+
+def close(out, ref, tol, what=""):
+    out = out.float().cpu()
+    ref = ref.float().cpu()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-12
+    assert err <= tol * scale, f"{what}: max|err| {err:.3e} > {tol:.1e} * {scale:.3e}"
+
+
+# ---------------------------------------------------------------------------------------------
+# GEMM
+# ---------------------------------------------------------------------------------------------
+GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("al,bl", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_layouts(M, N, K, al, bl):
+    if al == 1 and M % 8:
+        pytest.skip("a_layout 1 needs M % 8 == 0")
+    A = rnd((M, K), 1)
+    B = rnd((N, K), 2)
+    ref = A.float() @ B.float().T
+    Ad = (A if al == 0 else A.T.contiguous()).to(DEV)
+    Bd = (B if bl == 0 else B.T.contiguous()).to(DEV)
+    C = torch.empty((M, N), dtype=BF, device=DEV)
+    ops().gemm(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), C, N)
+    close(C, ref, 8e-3, f"gemm {al}{bl} {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_epilogues(act):
+    M, N, K = 300, 264, 192
+    x, w, b = rnd((M, K), 3), rnd((N, K), 4, 0.1), rnd((N,), 5, 0.1)
+    r = rnd((M, N), 6)
+    y, pre = ops().linear(x.to(DEV), w.to(DEV), b.to(DEV), act=act, residual=r.to(DEV), want_preact=True)
+    p = (x.float() @ w.float().T + b.float()).to(BF).float()
+    a = {0: p, 1: F.gelu(p), 2: O.quick_gelu(p)}[act]
+    close(pre, p, 8e-3, "preact")
+    close(y, a.to(BF).float() + r.float(), 8e-3, "epilogue")
+
+
+def test_gemm_f32_accumulate_beta():
+    M, N, K = 128, 192, 256
+    dy, x = rnd((M, N), 7), rnd((M, K), 8)
+    out = rnd((N, K), 9, dtype=torch.float32).to(DEV)
+    base = out.clone()
+    ops().linear_dw(dy.to(DEV), x.to(DEV), out, beta=1.0)
+    ref = dy.float().T @ x.float() + base.cpu()
+    close(out, ref, 1e-5, "dw beta f32")
+
+
+def test_linear_dx_dw_bf16():
+    M, N, K = 520, 384, 264
+    dy, w, x = rnd((M, N), 10), rnd((N, K), 11), rnd((M, K), 12)
+    dx = ops().linear_dx(dy.to(DEV), w.to(DEV))
+    close(dx, dy.float() @ w.float(), 8e-3, "dx")
+    dw = torch.empty((N, K), dtype=BF, device=DEV)
+    ops().linear_dw(dy.to(DEV), x.to(DEV), dw)
+    close(dw, dy.float().T @ x.float(), 8e-3, "dw")
+
+
+def test_gemm_strided_operands():
+    # q|k|v fused projection output consumed as strided views (ld > K)
+    M, K, N = 96, 128, 64
+    big = rnd((M, 3 * K), 13)
+    w = rnd((N, K), 14)
+    xv = big.to(DEV)[:, K:2 * K]
+    y = ops().linear(xv, w.to(DEV))
+    close(y, big[:, K:2 * K].float() @ w.float().T, 8e-3, "strided")
+
+
+# ---------------------------------------------------------------------------------------------
+# norms
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("rows,cols", [(64, 4096), (37, 1024), (5, 128), (9, 8192)])
+def test_rmsnorm(rows, cols):
+    x, w = rnd((rows, cols), 20), (1 + 0.1 * rnd((cols,), 21).float()).to(BF)
+    y, rstd = ops().rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = O.rmsnorm(xr, wr, 1e-5)
+    close(y, yr, 8e-3, "rms fwd")
+    dy = rnd((rows, cols), 22)
+    dres = rnd((rows, cols), 23)
+    dw = torch.empty(cols, dtype=torch.float32, device=DEV)
+    dx = ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV), dw=dw)
+    yr.backward(dy.float())
+    close(dx, xr.grad + dres.float(), 1e-2, "rms dx")
+    close(dw, wr.grad, 1e-2, "rms dw")
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 1024), (577, 128), (3, 64)])
+def test_layernorm(rows, cols):
+    x = rnd((rows, cols), 30, 2.0)
+    w, b = (1 + 0.1 * rnd((cols,), 31).float()).to(BF), rnd((cols,), 32, 0.1)
+    y, mean, rstd = ops().layernorm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1e-5)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.float().requires_grad_(True), b.float().requires_grad_(True)
+    yr = O.layernorm(xr, wr, br, 1e-5)
+    close(y, yr, 8e-3, "ln fwd")
+    dy = rnd((rows, cols), 33)
+    dw = torch.empty(cols, dtype=torch.float32, device=DEV)
+    db = torch.empty(cols, dtype=torch.float32, device=DEV)
+    dx = ops().layernorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), mean, rstd, dw=dw, db=db)
+    yr.backward(dy.float())
+    close(dx, xr.grad, 1e-2, "ln dx")
+    close(dw, wr.grad, 1e-2, "ln dw")
+    close(db, br.grad, 1e-3, "ln db")
+
+
+# ---------------------------------------------------------------------------------------------
+# element-wise
+# ---------------------------------------------------------------------------------------------
+def test_swiglu():
+    rows, Fd = 70, 688
+    gu = rnd((rows, 2 * Fd), 40, 2.0)
+    out = ops().swiglu_fwd(gu.to(DEV))
+    g, u = gu[:, :Fd].float().requires_grad_(True), gu[:, Fd:].float().requires_grad_(True)
+    ref = F.silu(g) * u
+    close(out, ref, 8e-3, "swiglu")
+    d = rnd((rows, Fd), 41)
+    dgu = ops().swiglu_bwd(d.to(DEV), gu.to(DEV))
+    ref.backward(d.float())
+    close(dgu[:, :Fd], g.grad, 1e-2, "dgate")
+    close(dgu[:, Fd:], u.grad, 1e-2, "dup")
+
+
+@pytest.mark.parametrize("act", [1, 2])
+def test_act_bwd(act):
+    x = rnd((33, 256), 50, 2.0)
+    dy = rnd((33, 256), 51)
+    xr = x.float().requires_grad_(True)
+    (F.gelu(xr) if act == 1 else O.quick_gelu(xr)).backward(dy.float())
+    dx = ops().act_bwd(act, dy.to(DEV), x.to(DEV))
+    close(dx, xr.grad, 8e-3, "act bwd")
+
+
+def test_colsum():
+    x = rnd((1000, 264), 55)
+    out = torch.zeros(264, dtype=torch.float32, device=DEV)
+    ops().colsum(x.to(DEV), out)
+    close(out, x.float().sum(0), 1e-5, "colsum")
+
+
+@pytest.mark.parametrize("D,H", [(128, 4), (64, 3)])
+def test_rope(D, H):
+    T = 50
+    q = rnd((T, H * D), 60)
+    k = rnd((T, H * D), 61)
+    pos = torch.randint(0, 1100, (T,))
+    cos, sin = O.rope_cos_sin(pos[None], D, 10000.0)
+    cos, sin = cos.to(BF).float(), sin.to(BF).float()
+    def ref(x):
+        xh = x.float().view(1, T, H, D).transpose(1, 2)
+        return O.apply_rope(xh, cos, sin).transpose(1, 2).reshape(T, H * D)
+    qd, kd = q.to(DEV), k.to(DEV)
+    ops().rope(qd, kd, pos.to(DEV), hq=H, hk=H, head_dim=D, theta=10000.0)
+    close(qd, ref(q), 8e-3, "rope q")
+    close(kd, ref(k), 8e-3, "rope k")
+    ops().rope(qd, kd, pos.to(DEV), hq=H, hk=H, head_dim=D, theta=10000.0, inverse=True)
+    close(qd, q.float(), 2e-2, "rope inverse")
+
+
+# ---------------------------------------------------------------------------------------------
+# attention
+# ---------------------------------------------------------------------------------------------
+ATTN = [
+    # B, H, L, D, causal
+    (2, 2, 200, 128, True),
+    (1, 3, 1088, 128, True),
+    (2, 2, 577, 64, False),
+    (1, 2, 64, 64, False),
+    (1, 1, 33, 128, False),
+]
+
+
+def _attn_ref(q, k, v, B, H, L, D, causal, kv_start=None):
+    qf = q.float().view(B, L, H, D).transpose(1, 2).requires_grad_(True)
+    kf = k.float().view(B, L, H, D).transpose(1, 2).requires_grad_(True)
+    vf = v.float().view(B, L, H, D).transpose(1, 2).requires_grad_(True)
+    allowed = None
+    if causal:
+        m = torch.ones(B, L, dtype=torch.long)
+        if kv_start is not None:
+            for b, s in enumerate(kv_start):
+                m[b, :s] = 0
+        allowed = O.causal_allowed(m)
+    o = O.attention(qf, kf, vf, D ** -0.5, allowed)
+    return qf, kf, vf, o
+
+
+@pytest.mark.parametrize("B,H,L,D,causal", ATTN)
+def test_attention_fwd_bwd(B, H, L, D, causal):
+    q, k, v = rnd((B * L, H * D), 70), rnd((B * L, H * D), 71), rnd((B * L, H * D), 72)
+    qf, kf, vf, o_ref = _attn_ref(q, k, v, B, H, L, D, causal)
+    o, lse = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
+                            causal=causal)
+    o_ref2 = o_ref.transpose(1, 2).reshape(B * L, H * D)
+    close(o, o_ref2, 1.2e-2, "attn o")
+    s = (qf @ kf.transpose(-1, -2)) * D ** -0.5
+    if causal:
+        s = s.masked_fill(~torch.ones(L, L, dtype=torch.bool).tril(), float("-inf"))
+    close(lse, torch.logsumexp(s, -1), 1e-3, "attn lse")
+    do = rnd((B * L, H * D), 73)
+    o_ref2.backward(do.float())
+    dq, dk, dv = ops().attn_bwd(q.to(DEV), k.to(DEV), v.to(DEV), o, do.to(DEV), lse, B=B, H=H, Lq=L, Lk=L, D=D,
+                                scale=D ** -0.5, causal=causal)
+    tr = lambda g: g.transpose(1, 2).reshape(B * L, H * D)
+    close(dv, tr(vf.grad), 2e-2, "dv")
+    close(dk, tr(kf.grad), 2e-2, "dk")
+    close(dq, tr(qf.grad), 2e-2, "dq")
+
+
+def test_attention_strided_and_kv_start():
+    B, H, L, D = 2, 2, 160, 128
+    qkv = rnd((B * L, 3 * H * D), 80)
+    kv_start = [0, 37]
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    qf, kf, vf, o_ref = _attn_ref(q.contiguous(), k.contiguous(), v.contiguous(), B, H, L, D, True, kv_start)
+    d = qkv.to(DEV)
+    ks = torch.tensor(kv_start, dtype=torch.int32, device=DEV)
+    o, lse = ops().attn_fwd(d[:, :H * D], d[:, H * D:2 * H * D], d[:, 2 * H * D:], B=B, H=H, Lq=L, Lk=L, D=D,
+                            scale=D ** -0.5, causal=True, kv_start=ks)
+    ref = o_ref.transpose(1, 2).reshape(B * L, H * D)
+    valid = torch.ones(B * L, dtype=torch.bool)
+    valid[L:L + 37] = False  # fully masked query rows of batch 1
+    close(o.cpu()[valid], ref[valid], 1.2e-2, "strided attn")
+
+
+# ---------------------------------------------------------------------------------------------
+# embeddings / merge / loss
+# ---------------------------------------------------------------------------------------------
+def test_embedding_fwd_bwd_exact():
+    V, Dm, n = 500, 256, 300
+    table = rnd((V, Dm), 90)
+    ids = torch.randint(0, V, (n,))
+    ids[::7] = 3  # duplicates
+    out = ops().embedding_fwd(ids.to(DEV), table.to(DEV))
+    assert torch.equal(out.cpu(), table[ids])
+    dout = rnd((n, Dm), 91)
+    dt = torch.zeros((V, Dm), dtype=torch.float32, device=DEV)
+    ops().embedding_bwd(ids.to(DEV), dout.to(DEV), dt, beta=1.0)
+    ref = torch.zeros(V, Dm).index_add_(0, ids, dout.float())
+    close(dt, ref, 1e-6, "embedding bwd")
+
+
+@pytest.mark.parametrize("pad_tail,left", [(None, False), ([0, 5], False), ([0, 6], True)])
+def test_merge_plan_bit_exact(pad_tail, left):
+    cfg = O.config_small_gpu()
+    ids, mask, _, _ = O.make_inputs(cfg, 2, 40, 4, 3, pad_tail=pad_tail)
+    if left and pad_tail:  # move padding to the front
+        for b, n in enumerate(pad_tail):
+            if n:
+                ids[b] = torch.cat([ids[b, 40 - n:], ids[b, :40 - n]])
+                mask[b] = torch.cat([mask[b, 40 - n:], mask[b, :40 - n]])
+    P, D = cfg.vision.num_patches, 16
+    emb = rnd((2, 40, D), 95)
+    img = rnd((2, P, D), 96)
+    r_emb, r_mask, _, r_pos = O.merge(img, emb, ids, mask, cfg)
+    L = r_emb.shape[1]
+    left_pad = not bool((ids[:, -1] == cfg.pad_token_id).sum())
+    td, src, mm, pos = ops().merge_plan(ids.to(DEV), mask.to(DEV), L=L, image_token=cfg.image_token_index,
+                                       n_patches=P, left_padding=left_pad)
+    out = ops().row_gather2(src.reshape(-1), emb.to(DEV).reshape(-1, D), img.to(DEV).reshape(-1, D))
+    assert torch.equal(out.cpu().view(2, L, D), r_emb)
+    assert torch.equal(mm.cpu(), r_mask.long())
+    assert torch.equal(pos.cpu(), r_pos)
+
+
+def test_ce_fwd_bwd():
+    B, L, V = 2, 50, 1000
+    logits = rnd((B * L, V), 100, 3.0)
+    labels = torch.randint(0, V, (B, L))
+    labels[:, :10] = -100
+    mask = torch.ones(B, L, dtype=torch.long)
+    mask[1, 40:] = 0
+    tgt = ops().shift_targets(labels.to(DEV), mask.to(DEV))
+    ref_tgt = torch.full((B, L), -100)
+    ref_tgt[:, :-1] = torch.where(mask[:, 1:] != 0, labels[:, 1:], torch.tensor(-100))
+    assert torch.equal(tgt.cpu(), ref_tgt.reshape(-1))
+    lg = logits.to(DEV)
+    row_loss, lse = ops().ce_fwd(lg, tgt)
+    out = ops().ce_reduce(row_loss, tgt)
+    lr = logits.float().requires_grad_(True)
+    ref = O.shifted_ce(lr.view(B, L, V), labels, mask)
+    assert abs(out[0].item() - ref.item()) < 1e-5 * abs(ref.item()) + 1e-6
+    ref.backward()
+    d = ops().ce_bwd(lg, tgt, lse, out)
+    close(d, lr.grad, 8e-3, "ce bwd")
+
+
+def test_vision_front_end():
+    cfg = O.config_small_gpu().vision
+    B = 2
+    W = O.make_weights(O.config_small_gpu(), 5)
+    vp = "vision_tower.vision_model."
+    pix = torch.randn(B, 3, cfg.image_size, cfg.image_size, generator=torch.Generator().manual_seed(7))
+    kpad = 640
+    patches = ops().im2col_patches(pix.to(DEV), cfg.patch_size, kpad)
+    wconv = W[vp + "embeddings.patch_embedding.weight"].reshape(cfg.hidden_size, -1)
+    wpad = torch.zeros(cfg.hidden_size, kpad)
+    wpad[:, :wconv.shape[1]] = wconv
+    x = ops().linear(patches, wpad.to(BF).to(DEV))
+    T = cfg.num_patches + 1
+    bf = lambda t: t.to(BF).to(DEV)
+    h = ops().vision_embed_ln(x, bf(W[vp + "embeddings.class_embedding"]),
+                              bf(W[vp + "embeddings.position_embedding.weight"]), bf(W[vp + "pre_layrnorm.weight"]),
+                              bf(W[vp + "pre_layrnorm.bias"]), B=B, T=T, eps=cfg.layer_norm_eps)
+    ref = O.vision_hidden_states(pix, W, cfg, 0)[0]
+    close(h.view(B, T, -1), ref, 2e-2, "vision embed+ln")
+
+
+def test_adamw_matches_torch():
+    n = 4096 + 24
+    p0 = rnd((n,), 110, dtype=torch.float32)
+    grads = [rnd((n,), 111 + i, dtype=torch.float32) for i in range(3)]
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-2, weight_decay=0.1)
+    p = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for step, g in enumerate(grads, 1):
+        ref.grad = g.clone()
+        opt.step()
+        ops().adamw(p, g.to(DEV), m, v, lr=1e-2, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.1, step=step)
+    close(p, ref.detach(), 1e-5, "adamw")
+
+
+def test_clip_coef_and_sumsq():
+    a = rnd((1000,), 120, dtype=torch.float32).to(DEV)
+    b = rnd((333,), 121).to(DEV)
+    acc = torch.zeros(1, device=DEV)
+    ops().sumsq(a, acc)
+    ops().sumsq(b, acc)
+    norm = math.sqrt(a.double().pow(2).sum().item() + b.double().pow(2).sum().item())
+    coef = torch.empty(1, device=DEV)
+    nrm = torch.empty(1, device=DEV)
+    ops().clip_coef(acc, 1.0, coef, nrm)
+    assert abs(nrm.item() - norm) < 1e-4 * norm
+    assert abs(coef.item() - min(1.0, 1.0 / (norm + 1e-6))) < 1e-6
