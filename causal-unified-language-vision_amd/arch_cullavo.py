@@ -1,0 +1,191 @@
+"""CuLLaVOModel: drop-in for the reference's model class (reference cullavo/arch_cullavo.py:24,
+546-677) whose dense math runs on the gfx950 kernels.
+
+Same constructor-visible structure (.vision_tower, .multi_modal_projector, .language_model with
+.model/.lm_head, .get_input_embeddings(), .config), same forward signature, same
+CullavoCausalLMOutputWithPast result (tuple form when return_dict=False) and the same
+ValueError for an unknown vision_feature_select_strategy.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, fields
+from typing import Optional, Tuple
+
+import torch
+from torch import nn
+
+from . import ops
+from .config import CuLLaVOConfig
+from .functions import HeadLossFn, MergeFn, StepContext
+from .modeling import (CLIPVisionModel, LlamaForCausalLM, LlavaMultiModalProjector, build_arenas, init_random_)
+
+
+@dataclass
+class CullavoCausalLMOutputWithPast:
+    """reference cullavo/arch_cullavo.py:14-21"""
+    loss: Optional[torch.Tensor] = None
+    logits: torch.Tensor = None
+    past_key_values: Optional[list] = None
+    hidden_states: Optional[Tuple[torch.Tensor]] = None
+    attentions: Optional[Tuple[torch.Tensor]] = None
+    image_hidden_states: Optional[Tuple[torch.Tensor]] = None
+
+    def __getitem__(self, k):
+        if isinstance(k, str):
+            return getattr(self, k)
+        return self.to_tuple()[k]
+
+    def to_tuple(self):
+        return tuple(getattr(self, f.name) for f in fields(self) if getattr(self, f.name) is not None)
+
+
+class CuLLaVOModel(nn.Module):
+    def __init__(self, config: CuLLaVOConfig, *, device="cuda", trainable: str = "full", init: str = "random",
+                 seed: int = 0):
+        super().__init__()
+        if config.vision_config.hidden_act != "quick_gelu" or config.projector_hidden_act != "gelu":
+            raise ValueError("CuLLaVO path: CLIP quick_gelu + projector gelu")
+        self.config = config
+        self.arenas = build_arenas(config, device, trainable)
+        if init == "random":
+            init_random_(self.arenas, seed)
+        self.vision_tower = CLIPVisionModel(config.vision_config, self.arenas["vision"])
+        self.multi_modal_projector = LlavaMultiModalProjector(self.arenas["projector"].params)
+        self.language_model = LlamaForCausalLM(config.text_config, self.arenas["embed"], self.arenas["layers"],
+                                               self.arenas["head"])
+        self.trainable_policy = trainable
+
+    # -- reference API -------------------------------------------------------------------------
+    def get_input_embeddings(self):
+        return self.language_model.model.embed_tokens
+
+    def get_output_embeddings(self):
+        return self.language_model.lm_head
+
+    def to(self, *a, **k):  # parameters are views into HBM arenas: moving would break them
+        raise RuntimeError("CuLLaVOModel lives where it was built (pass device= to the constructor)")
+
+    def zero_grad(self, set_to_none: bool = False):
+        for ar in self.arenas.values():
+            ar.zero_grad()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """Load llava-hf (transformers ~4.37) keys; copies into the arenas in place."""
+        own = {}
+        for ar in self.arenas.values():
+            own.update(ar.params)
+        missing = [k for k in own if k not in state_dict]
+        unexpected = [k for k in state_dict if k not in own]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"load_state_dict: missing {missing[:5]}..., unexpected {unexpected[:5]}...")
+        with torch.no_grad():
+            for k, v in state_dict.items():
+                if k in own:
+                    own[k].copy_(v.to(own[k].dtype))
+        return missing, unexpected
+
+    def state_dict(self, *a, **k):
+        out = {}
+        for ar in self.arenas.values():
+            out.update({key: p.detach() for key, p in ar.params.items()})
+        return out
+
+    # -- forward (reference cullavo/arch_cullavo.py:546-677) ------------------------------------
+    def forward(self, input_ids=None, pixel_values=None, attention_mask=None, position_ids=None, past_key_values=None,
+                inputs_embeds=None, vision_feature_layer=None, vision_feature_select_strategy=None, labels=None,
+                use_cache=None, output_attentions=None, output_hidden_states=None, return_dict=None):
+        cfg = self.config
+        output_hidden_states = output_hidden_states if output_hidden_states is not None else cfg.output_hidden_states
+        return_dict = return_dict if return_dict is not None else cfg.use_return_dict
+        vision_feature_layer = vision_feature_layer if vision_feature_layer is not None else cfg.vision_feature_layer
+        strategy = (vision_feature_select_strategy if vision_feature_select_strategy is not None
+                    else cfg.vision_feature_select_strategy)
+        if past_key_values is not None or use_cache:
+            raise NotImplementedError("KV-cache decode / generate is SURVEY.md §8(f) row 2 (not built yet)")
+        if output_attentions:
+            raise NotImplementedError("flash attention never materialises attention probabilities")
+
+        self.vision_tower.eval()  # :578 (no dropout in this tower; kept for parity of intent)
+
+        if inputs_embeds is None:
+            B, S = input_ids.shape
+            inputs_embeds = self.get_input_embeddings()(input_ids)  # :582
+            if pixel_values is not None and S != 1:
+                image_features = self._image_features(pixel_values, vision_feature_layer, strategy)  # :586-599
+                inputs_embeds, attention_mask, position_ids = self._merge(image_features, inputs_embeds, input_ids,
+                                                                          attention_mask)  # :600-602
+                if labels is None:  # :603-604
+                    labels = torch.full_like(attention_mask, cfg.ignore_index).to(torch.long)
+        B, L, d = inputs_embeds.shape
+        if position_ids is None:
+            position_ids = torch.arange(L, device=inputs_embeds.device).expand(B, L)
+        kv_start = None
+        if attention_mask is not None:
+            kv_start = (attention_mask.cumsum(-1) == 0).sum(-1).to(torch.int32)
+        sctx = StepContext(B, L, position_ids, kv_start)
+        lm = self.language_model
+        h, hs = lm.decode(inputs_embeds.reshape(B * L, d).contiguous(), sctx, bool(output_hidden_states))  # :638
+        loss = None
+        if labels is not None:  # :651-665
+            targets = ops.shift_targets(labels, attention_mask, cfg.ignore_index)
+            loss, logits = HeadLossFn.apply(h, lm, targets, cfg.ignore_index, *lm.head_params())
+        else:
+            logits = lm.lm_head(lm.model.norm(h))
+        logits = logits.view(B, L, -1)
+        hs_t = tuple(t.view(B, L, d) for t in hs) if hs else None
+        if not return_dict:  # :667-669
+            out = (logits,) + ((hs_t,) if hs_t is not None else ())
+            return (loss,) + out if loss is not None else out
+        return CullavoCausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=None, hidden_states=hs_t,
+                                             attentions=None)
+
+    # -- pieces ---------------------------------------------------------------------------------
+    def _image_features(self, pixel_values, layer: int, strategy: str):
+        vt = self.vision_tower.vision_model
+        n = vt.cfg.num_hidden_layers
+        idx = n + 1 + layer if layer < 0 else layer
+        if not 0 <= idx <= n:
+            raise IndexError(f"vision_feature_layer {layer} out of range")
+        feats = vt.hidden_state(pixel_values, idx)  # hidden_states[layer], only the layers needed
+        if strategy == "default":
+            feats = feats[:, 1:]
+        elif strategy == "full":
+            pass
+        else:
+            raise ValueError(f"Unexpected select feature strategy: {self.config.vision_feature_select_strategy}")
+        return self.multi_modal_projector(feats)
+
+    def _merge(self, image_features, inputs_embeds, input_ids, attention_mask):
+        """transformers ~4.37 _merge_input_ids_with_image_features on the merge_plan kernel.
+        One small device->host read (image-token counts, left-padding flag) sizes the output,
+        as the reference's .max() / torch.where do."""
+        cfg = self.config
+        n_img, P, d = image_features.shape
+        B, S = input_ids.shape
+        is_img = input_ids == cfg.image_token_index
+        stats = torch.stack([is_img.sum(-1).max(), is_img.sum(), (input_ids[:, -1] == cfg.pad_token_id).sum()]).cpu()
+        n_max, n_total, n_pad_last = (int(x) for x in stats)
+        if n_total != n_img:
+            raise ValueError(f"The input provided to the model are wrong. The number of image tokens is {n_total} "
+                             f"while the number of image given to the model is {n_img}. This prevents correct "
+                             f"indexing and breaks batch generation.")
+        left_padding = n_pad_last == 0
+        L = n_max * (P - 1) + S
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        text_dst, src, mmask, pos = ops.merge_plan(input_ids, attention_mask, L=L, image_token=cfg.image_token_index,
+                                                   n_patches=P, left_padding=left_padding)
+        n_text = B * S
+        flat = src.reshape(-1)
+        rows = torch.arange(B * L, device=flat.device)
+        is_img_row = flat >= n_text
+        img_dst = torch.empty(n_img * P + 1, dtype=torch.int64, device=flat.device)
+        img_dst.scatter_(0, torch.where(is_img_row, flat - n_text, n_img * P), rows)
+        merged = MergeFn.apply(inputs_embeds.reshape(n_text, d), image_features.reshape(n_img * P, d), flat,
+                               text_dst, img_dst[:-1])
+        return merged.view(B, L, d), mmask, pos
+
+
+def build_cullavo(config: CuLLaVOConfig | None = None, **kw) -> CuLLaVOModel:
+    from .config import llava_1_5_7b
+    return CuLLaVOModel(config or llava_1_5_7b(), **kw)

@@ -1,0 +1,113 @@
+"""Flat parameter / gradient arenas.
+
+Every parameter group (vision tower, projector, token embedding, decoder layers, lm_head) lives
+in ONE contiguous bf16 buffer, with the parameters as views into it, laid out so that
+the q|k|v projections of a layer and its gate|up projections are adjacent: the fused
+[3d, d] / [2F, d] weight of a single GEMM is then just another view (no copies, no
+re-packing). Trainable groups own a matching flat gradient buffer; the backward GEMMs write
+dW straight into it (beta = 0 on the first write of an accumulation cycle, 1 after), the DP
+all-reduce works on contiguous slices of it, and AdamW runs over the whole buffer in one
+kernel. 288 GB of HBM makes this trade (no compaction, everything resident) the right one.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+
+class ParamArena:
+    def __init__(self, name: str, specs: list[tuple[str, tuple[int, ...]]], *, device, dtype=torch.bfloat16,
+                 trainable: bool = False):
+        self.name = name
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.offsets: dict[str, tuple[int, int, tuple[int, ...]]] = {}
+        off = 0
+        for key, shape in specs:
+            n = int(math.prod(shape))
+            self.offsets[key] = (off, n, tuple(shape))
+            off += n
+        self.numel = off
+        self.flat = torch.empty(off, dtype=dtype, device=self.device)
+        self.params: dict[str, nn.Parameter] = {}
+        for key, (o, n, shape) in self.offsets.items():
+            p = nn.Parameter(self.flat[o:o + n].view(shape), requires_grad=trainable)
+            p._cv_arena = self
+            p._cv_key = key
+            self.params[key] = p
+        self.trainable = trainable
+        self.grad_flat = None
+        self._written: set[str] = set()
+        if trainable:
+            self.grad_flat = torch.zeros(off, dtype=dtype, device=self.device)
+            self._attach_grads()
+
+    # -- views -----------------------------------------------------------------------------
+    def view(self, first_key: str, n_keys_shape: tuple[int, ...], *, grad: bool = False) -> torch.Tensor:
+        """A view starting at first_key spanning prod(shape) elements (fused weights)."""
+        o = self.offsets[first_key][0]
+        n = int(math.prod(n_keys_shape))
+        buf = self.grad_flat if grad else self.flat
+        return buf[o:o + n].view(n_keys_shape)
+
+    def check_adjacent(self, keys: list[str]):
+        for a, b in zip(keys, keys[1:]):
+            oa, na, _ = self.offsets[a]
+            if self.offsets[b][0] != oa + na:
+                raise RuntimeError(f"arena {self.name}: {a} and {b} are not adjacent")
+
+    def slice_of(self, keys: list[str]) -> tuple[int, int]:
+        lo = min(self.offsets[k][0] for k in keys)
+        hi = max(self.offsets[k][0] + self.offsets[k][1] for k in keys)
+        return lo, hi
+
+    # -- gradients ---------------------------------------------------------------------------
+    def _attach_grads(self):
+        for key, (o, n, shape) in self.offsets.items():
+            self.params[key].grad = self.grad_flat[o:o + n].view(shape)
+
+    def grad_slot(self, key: str, span: tuple[int, ...] | None = None) -> tuple[torch.Tensor, float]:
+        """(gradient view to write, beta): beta=0 on the first write in this accumulation
+        cycle, 1 afterwards. `span` widens the view over adjacent keys (fused weights)."""
+        if not self.trainable:
+            raise RuntimeError(f"arena {self.name} is frozen")
+        if self.params[key].grad is None:  # e.g. optimizer.zero_grad(set_to_none=True)
+            self._attach_grads()
+        beta = 1.0 if key in self._written else 0.0
+        self._written.add(key)
+        if span is None:
+            o, n, shape = self.offsets[key]
+            return self.grad_flat[o:o + n].view(shape), beta
+        return self.view(key, span, grad=True), beta
+
+    def mark_written(self, keys: list[str]):
+        self._written.update(keys)
+
+    def zero_grad(self):
+        """Start a new accumulation cycle. Buffers are not cleared: the first backward write
+        uses beta = 0. Parameters that were never written last cycle are zeroed explicitly."""
+        if self.trainable:
+            unwritten = [k for k in self.offsets if k not in self._written]
+            for k in unwritten:
+                o, n, _ = self.offsets[k]
+                self.grad_flat[o:o + n].zero_()
+            self._attach_grads()
+        self._written = set()
+
+    def finalize_grads(self):
+        """Zero the gradient of every parameter that received no write this cycle."""
+        if self.trainable:
+            for k, (o, n, _) in self.offsets.items():
+                if k not in self._written:
+                    self.grad_flat[o:o + n].zero_()
+                    self._written.add(k)
+
+
+def grad_slot(p: nn.Parameter, span=None):
+    return p._cv_arena.grad_slot(p._cv_key, span)
+
+
+def trainable(p) -> bool:
+    return p is not None and p.requires_grad

@@ -263,7 +263,9 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
   CV_REQUIRE(a_layout == 0 || a_layout == 1, CULLAVO_EINVAL, "a_layout");
   CV_REQUIRE(b_layout == 0 || b_layout == 1, CULLAVO_EINVAL, "b_layout");
   CV_REQUIRE(M >= 0 && N >= 0 && K >= 0, CULLAVO_EINVAL, "negative size");
-  CV_REQUIRE(K % 8 == 0 && N % 8 == 0, CULLAVO_EINVAL, "K and N must be multiples of 8");
+  CV_REQUIRE(N % 8 == 0, CULLAVO_EINVAL, "N must be a multiple of 8");
+  CV_REQUIRE((a_layout == 1 && b_layout == 1) || K % 8 == 0, CULLAVO_EINVAL,
+             "K must be a multiple of 8 when an operand is K-contiguous");
   CV_REQUIRE(a_layout == 0 || M % 8 == 0, CULLAVO_EINVAL, "M must be a multiple of 8 for a_layout 1");
   CV_REQUIRE(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 && (residual == nullptr || ldr % 8 == 0),
              CULLAVO_EINVAL, "leading dimensions must be multiples of 8");

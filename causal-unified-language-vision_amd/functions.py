@@ -1,0 +1,318 @@
+"""Autograd Functions of the hot path. Each one runs a whole block of the reference's module
+chain on the C-ABI kernels and has a hand-written backward that writes parameter gradients
+straight into the arena (arena.grad_slot) and returns only activation gradients.
+
+  LinearFn          nn.Linear (any Linear called on its own)
+  LlamaLayerFn      LlamaDecoderLayer   tf:models/llama/modeling_llama.py:284-345
+  ClipLayerFn       CLIPEncoderLayer    tf:models/clip/modeling_clip.py:353-384
+  ProjectorFn       LlavaMultiModalProjector tf:models/llava/modeling_llava.py:87-107
+  EmbeddingFn       embed_tokens        reference cullavo/arch_cullavo.py:582
+  MergeFn           _merge_input_ids_with_image_features rows   arch_cullavo.py:600-602
+  HeadLossFn        final RMSNorm + lm_head + shifted masked CE   arch_cullavo.py:651-665
+
+Parameters are passed to .apply only so autograd sees a dependency; their returned gradient
+is None (the value is already in the arena).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .arena import grad_slot, trainable
+from .ops import ACT_GELU, ACT_QUICK_GELU
+
+
+def _needs_grad(ctx) -> bool:
+    # grad mode is off inside Function.forward; needs_input_grad says whether backward will run
+    return any(ctx.needs_input_grad)
+
+
+def _lin_act(x, w, b, act, keep_preact):
+    if keep_preact:
+        return ops.linear(x, w, b, act=act, want_preact=True)
+    return ops.linear(x, w, b, act=act), None
+
+
+def _write_dw(dy, x, w):
+    if trainable(w):
+        g, beta = grad_slot(w)
+        ops.linear_dw(dy, x, g, beta=beta)
+
+
+def _write_bias(dy, b):
+    if trainable(b):
+        g, beta = grad_slot(b)
+        ops.colsum(dy, g, beta=beta)
+
+
+# ---------------------------------------------------------------------------------------------
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        y = ops.linear(x2, w, b)
+        ctx.save_for_backward(x2, w, b)
+        ctx.shp = shp
+        return y.view(*shp[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0]).contiguous()
+        _write_dw(dy2, x2, w)
+        _write_bias(dy2, b)
+        dx = ops.linear_dx(dy2, w).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        return dx, None, None
+
+
+# ---------------------------------------------------------------------------------------------
+class StepContext:
+    """Per-forward shape/index state shared by the decoder layers (built once per step)."""
+
+    def __init__(self, B: int, L: int, position_ids, kv_start=None):
+        self.B, self.L = B, L
+        self.position_ids = position_ids.reshape(-1).contiguous()
+        self.kv_start = kv_start
+
+
+class LlamaLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, layer, sctx: StepContext, *params):
+        cfg = layer.cfg
+        T, d = h.shape
+        H, D = cfg.num_attention_heads, cfg.head_dim
+        Fd = cfg.intermediate_size
+        grad = _needs_grad(ctx)
+        x1, rstd1 = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
+        qkv = ops.linear(x1, layer.w_qkv())  # [T, 3d]: q | k | v
+        q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+        ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
+        o, lse = ops.attn_fwd(q, k, v, B=sctx.B, H=H, Lq=sctx.L, Lk=sctx.L, D=D, scale=D ** -0.5, causal=True,
+                              kv_start=sctx.kv_start)
+        h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h)
+        x2, rstd2 = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
+        gu = ops.linear(x2, layer.w_gu())  # [T, 2F]: gate | up
+        a = ops.swiglu_fwd(gu)
+        h3 = ops.linear(a, layer.mlp.down_proj.weight, residual=h2)
+        if grad:
+            ctx.layer, ctx.sctx = layer, sctx
+            ctx.saved = (h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a)
+        return h3
+
+    @staticmethod
+    def backward(ctx, dh3):
+        layer, sctx = ctx.layer, ctx.sctx
+        cfg = layer.cfg
+        h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a = ctx.saved
+        ctx.saved = None
+        T, d = h.shape
+        H, D = cfg.num_attention_heads, cfg.head_dim
+        dh3 = dh3.contiguous()
+        # MLP
+        da = ops.linear_dx(dh3, layer.mlp.down_proj.weight)
+        _write_dw(dh3, a, layer.mlp.down_proj.weight)
+        dgu = ops.swiglu_bwd(da, gu)
+        del da
+        dx2 = ops.linear_dx(dgu, layer.w_gu())
+        if trainable(layer.mlp.gate_proj.weight):
+            g, beta = layer.gu_grad_slot()
+            ops.linear_dw(dgu, x2, g, beta=beta)
+        del dgu
+        wpost = layer.post_attention_layernorm.weight
+        dw_post, beta_post = grad_slot(wpost) if trainable(wpost) else (None, 0.0)
+        dh2 = ops.rmsnorm_bwd(dx2, h2, wpost, rstd2, dres=dh3, dw=dw_post, beta=beta_post)
+        del dx2
+        # attention
+        do = ops.linear_dx(dh2, layer.self_attn.o_proj.weight)
+        _write_dw(dh2, o, layer.self_attn.o_proj.weight)
+        dqkv = torch.empty_like(qkv)
+        q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+        ops.attn_bwd(q, k, v, o, do, lse, B=sctx.B, H=H, Lq=sctx.L, Lk=sctx.L, D=D, scale=D ** -0.5, causal=True,
+                     kv_start=sctx.kv_start, dq=dqkv[:, :d], dk=dqkv[:, d:2 * d], dv=dqkv[:, 2 * d:])
+        del do
+        ops.rope(dqkv[:, :d], dqkv[:, d:2 * d], sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta,
+                 inverse=True)
+        dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+        if trainable(layer.self_attn.q_proj.weight):
+            g, beta = layer.qkv_grad_slot()
+            ops.linear_dw(dqkv, x1, g, beta=beta)
+        del dqkv
+        win = layer.input_layernorm.weight
+        dw_in, beta_in = grad_slot(win) if trainable(win) else (None, 0.0)
+        dh = ops.rmsnorm_bwd(dx1, h, win, rstd1, dres=dh2, dw=dw_in, beta=beta_in)
+        return (dh, None, None) + (None,) * len(layer.fn_params())
+
+
+# ---------------------------------------------------------------------------------------------
+class ClipLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, layer, B: int, T: int, *params):
+        cfg = layer.cfg
+        d = cfg.hidden_size
+        H, D = cfg.num_attention_heads, cfg.head_dim
+        grad = _needs_grad(ctx)
+        sa, mlp = layer.self_attn, layer.mlp
+        x1, m1, r1 = ops.layernorm_fwd(h, layer.layer_norm1.weight, layer.layer_norm1.bias, cfg.layer_norm_eps)
+        qkv = ops.linear(x1, layer.w_qkv(), layer.b_qkv())
+        q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+        o, lse = ops.attn_fwd(q, k, v, B=B, H=H, Lq=T, Lk=T, D=D, scale=D ** -0.5, causal=False)
+        h2 = ops.linear(o, sa.out_proj.weight, sa.out_proj.bias, residual=h)
+        x2, m2, r2 = ops.layernorm_fwd(h2, layer.layer_norm2.weight, layer.layer_norm2.bias, cfg.layer_norm_eps)
+        a, pre = _lin_act(x2, mlp.fc1.weight, mlp.fc1.bias, ACT_QUICK_GELU, grad)
+        h3 = ops.linear(a, mlp.fc2.weight, mlp.fc2.bias, residual=h2)
+        if grad:
+            ctx.layer, ctx.B, ctx.T = layer, B, T
+            ctx.saved = (h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre)
+        return h3
+
+    @staticmethod
+    def backward(ctx, dh3):
+        layer, B, T = ctx.layer, ctx.B, ctx.T
+        cfg = layer.cfg
+        d = cfg.hidden_size
+        H, D = cfg.num_attention_heads, cfg.head_dim
+        h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre = ctx.saved
+        ctx.saved = None
+        sa, mlp = layer.self_attn, layer.mlp
+        dh3 = dh3.contiguous()
+        da = ops.linear_dx(dh3, mlp.fc2.weight)
+        _write_dw(dh3, a, mlp.fc2.weight)
+        _write_bias(dh3, mlp.fc2.bias)
+        dpre = ops.act_bwd(ACT_QUICK_GELU, da, pre)
+        dx2 = ops.linear_dx(dpre, mlp.fc1.weight)
+        _write_dw(dpre, x2, mlp.fc1.weight)
+        _write_bias(dpre, mlp.fc1.bias)
+        ln2 = layer.layer_norm2
+        dw2, db2, beta2 = _ln_slots(ln2)
+        dh2 = ops.layernorm_bwd(dx2, h2, ln2.weight, m2, r2, dres=dh3, dw=dw2, db=db2, beta=beta2)
+        do = ops.linear_dx(dh2, sa.out_proj.weight)
+        _write_dw(dh2, o, sa.out_proj.weight)
+        _write_bias(dh2, sa.out_proj.bias)
+        dqkv = torch.empty_like(qkv)
+        ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, B=B, H=H, Lq=T, Lk=T, D=D,
+                     scale=D ** -0.5, causal=False, dq=dqkv[:, :d], dk=dqkv[:, d:2 * d], dv=dqkv[:, 2 * d:])
+        dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+        if trainable(sa.q_proj.weight):
+            g, beta = layer.qkv_grad_slot()
+            ops.linear_dw(dqkv, x1, g, beta=beta)
+            gb, betab = layer.qkv_bias_grad_slot()
+            ops.colsum(dqkv, gb, beta=betab)
+        ln1 = layer.layer_norm1
+        dw1, db1, beta1 = _ln_slots(ln1)
+        dh = ops.layernorm_bwd(dx1, h, ln1.weight, m1, r1, dres=dh2, dw=dw1, db=db1, beta=beta1)
+        return (dh, None, None, None) + (None,) * len(layer.fn_params())
+
+
+def _ln_slots(ln):
+    if not trainable(ln.weight):
+        return None, None, 0.0
+    gw, beta = grad_slot(ln.weight)
+    gb, _ = grad_slot(ln.bias)
+    return gw, gb, beta
+
+
+# ---------------------------------------------------------------------------------------------
+class ProjectorFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, proj, *params):
+        l1, l2 = proj.linear_1, proj.linear_2
+        grad = _needs_grad(ctx)
+        a, pre = _lin_act(x, l1.weight, l1.bias, ACT_GELU, grad)
+        y = ops.linear(a, l2.weight, l2.bias)
+        if grad:
+            ctx.proj = proj
+            ctx.saved = (x, a, pre)
+            ctx.x_grad = x.requires_grad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        proj = ctx.proj
+        x, a, pre = ctx.saved
+        ctx.saved = None
+        l1, l2 = proj.linear_1, proj.linear_2
+        dy = dy.contiguous()
+        da = ops.linear_dx(dy, l2.weight)
+        _write_dw(dy, a, l2.weight)
+        _write_bias(dy, l2.bias)
+        dpre = ops.act_bwd(ACT_GELU, da, pre)
+        _write_dw(dpre, x, l1.weight)
+        _write_bias(dpre, l1.bias)
+        dx = ops.linear_dx(dpre, l1.weight) if ctx.x_grad else None
+        return (dx, None) + (None,) * len(proj.fn_params())
+
+
+# ---------------------------------------------------------------------------------------------
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight):
+        out = ops.embedding_fwd(ids, weight)
+        ctx.ids, ctx.weight = ids, weight
+        return out.view(*ids.shape, weight.shape[1])
+
+    @staticmethod
+    def backward(ctx, dout):
+        w = ctx.weight
+        if trainable(w):
+            g, beta = grad_slot(w)
+            if beta == 0.0:
+                g.zero_()
+            ops.embedding_bwd(ctx.ids, dout.reshape(-1, w.shape[1]).contiguous(), g, beta=1.0)
+        return None, None
+
+
+class MergeFn(torch.autograd.Function):
+    """out rows = text rows (text_dst) | image rows | zeros, from the merge plan."""
+
+    @staticmethod
+    def forward(ctx, text, image, src, text_dst, img_dst):
+        out = ops.row_gather2(src.reshape(-1), text, image)
+        ctx.idx = (text_dst, img_dst)
+        ctx.shapes = (text.shape, image.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        text_dst, img_dst = ctx.idx
+        ts, ims = ctx.shapes
+        dout = dout.contiguous()
+        dtext = ops.row_gather2(text_dst.reshape(-1), dout, None).view(ts) if ctx.needs_input_grad[0] else None
+        dimg = ops.row_gather2(img_dst, dout, None).view(ims) if ctx.needs_input_grad[1] else None
+        return dtext, dimg, None, None, None
+
+
+# ---------------------------------------------------------------------------------------------
+class HeadLossFn(torch.autograd.Function):
+    """final RMSNorm -> lm_head -> per-row CE over shifted, masked targets -> mean."""
+
+    @staticmethod
+    def forward(ctx, h, lm, targets, ignore_index: int, *params):
+        norm_w, W = lm.model.norm.weight, lm.lm_head.weight
+        eps = lm.cfg.rms_norm_eps
+        x, rstd = ops.rmsnorm_fwd(h, norm_w, eps)
+        logits = ops.linear(x, W)
+        row_loss, lse = ops.ce_fwd(logits, targets, ignore_index)
+        out = ops.ce_reduce(row_loss, targets, ignore_index)
+        ctx.lm = lm
+        ctx.ignore = ignore_index
+        ctx.saved = (h, x, rstd, logits, targets, lse, out)
+        ctx.stats = out  # [loss, count, 1/count] on device (no host sync)
+        return out[0].clone(), logits
+
+    @staticmethod
+    def backward(ctx, dloss, dlogits):
+        lm = ctx.lm
+        h, x, rstd, logits, targets, lse, out = ctx.saved
+        ctx.saved = None
+        norm_w, W = lm.model.norm.weight, lm.lm_head.weight
+        gl = dloss.reshape(1).float().contiguous() if dloss is not None else torch.zeros(1, device=h.device)
+        dl = ops.ce_bwd(logits, targets, lse, out, gl, ctx.ignore)
+        if dlogits is not None:
+            dl += dlogits
+        dx = ops.linear_dx(dl, W)
+        _write_dw(dl, x, W)
+        del dl
+        dw, beta = grad_slot(norm_w) if trainable(norm_w) else (None, 0.0)
+        dh = ops.rmsnorm_bwd(dx, h, norm_w, rstd, dw=dw, beta=beta) if ctx.needs_input_grad[0] else None
+        return (dh, None, None, None) + (None,) * len(lm.head_params())

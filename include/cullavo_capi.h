@@ -51,6 +51,7 @@ const char* cullavo_last_error(void);
  * a_layout 1: A stored [K,M] (M contiguous, lda >= M)      -- dW = dY^T X
  * b_layout 0: B stored [N,K] (K contiguous, nn.Linear.weight)
  * b_layout 1: B stored [K,N] (N contiguous)                -- dX = dY W
+ * N % 8 == 0; K % 8 == 0 unless both layouts are 1; M % 8 == 0 for a_layout 1.
  * Replaces every nn.Linear of CLIP / projector / Llama (tf:clip/modeling_clip.py:280-351,
  * tf:llava/modeling_llava.py:87-107, tf:llama/modeling_llama.py:163-282, lm_head :480) and their
  * autograd backward. A,B,residual,bias,preact are bf16; C is bf16 or f32 (c_dtype).

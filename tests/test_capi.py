@@ -28,7 +28,7 @@ def test_nm_exports_match_header():
 
 def test_validation_errors_surface_without_gpu():
     # K not a multiple of 8 is rejected on the host before any launch
-    with pytest.raises(ValueError, match="multiples of 8"):
+    with pytest.raises(ValueError, match="multiple of 8"):
         _lib.call("gemm", 0, 0, 16, 16, 12, None, 12, None, 12, None, 16, 1, 1.0, None, 0, None, None, 0, 0.0, None)
     with pytest.raises(ValueError, match="head_dim"):
         _lib.call("rope", None, 128, None, 128, None, 4, 1, 1, 12, 10000.0, 0, 1, None)

@@ -369,3 +369,12 @@ def test_clip_coef_and_sumsq():
     ops().clip_coef(acc, 1.0, coef, nrm)
     assert abs(nrm.item() - norm) < 1e-4 * norm
     assert abs(coef.item() - min(1.0, 1.0 / (norm + 1e-6))) < 1e-6
+
+
+def test_linear_dw_ragged_token_count():
+    # dW reduces over tokens: B*L is arbitrary (590 here), only N % 8 matters
+    M, N, K = 590, 1024, 256
+    dy, x = rnd((M, N), 130), rnd((M, K), 131)
+    dw = torch.empty((N, K), dtype=torch.float32, device=DEV)
+    ops().linear_dw(dy.to(DEV), x.to(DEV), dw)
+    close(dw, dy.float().T @ x.float(), 1e-5, "dw ragged")
