@@ -1,0 +1,230 @@
+"""CuLLaVO train-step throughput on MI355X (BASELINE.json metric):
+"train-step samples/sec (336px img + 512-tok prompt, 7B LM) at 1/2/4/8 MI355X".
+
+A step = one full training step of CuLLaVOModel (llava-1.5-7b: CLIP ViT-L/14-336 + Vicuna-7B)
+on one synthetic batch resident in HBM: vision forward (frozen), projector, merge, 32 decoder
+layers, lm_head + shifted masked CE, the complete backward, bucketed RCCL gradient all-reduce
+(N>1), global-norm clip and fused AdamW. Per-GPU batch 8 (config 3; config 4 at N=8 = global
+64), weak scaling. Random-init weights (no checkpoints offline), synthetic data.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (see README / DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="samples per GPU")
+    ap.add_argument("--config", default="llava-1.5-7b")
+    ap.add_argument("--trainable", default="full", choices=["full", "reference"])
+    ap.add_argument("--text-len", type=int, default=513)
+    ap.add_argument("--bucket-mb", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, text_len: int, budget_s: float):
+    """The oracle (CPU fp32 restatement of the reference path) timed on this host's cores:
+    one Vicuna-7B decoder layer fwd+bwd, one CLIP-L/14 layer fwd, the lm_head fwd+bwd at B=1,
+    L=text_len+575; extrapolated to a full sample (x32 LM layers, x23 ViT layers)."""
+    import torch
+    from oracle import cullavo_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    ocfg = O.config_7b()
+    t, v = ocfg.text, ocfg.vision
+    L = text_len + v.num_patches - 1
+    g = torch.Generator().manual_seed(0)
+    d, f = t.hidden_size, t.intermediate_size
+    lp = "language_model.model.layers.0."
+    W = {lp + f"self_attn.{n}_proj.weight": torch.randn(d, d, generator=g) * d ** -0.5 for n in "qkvo"}
+    W[lp + "mlp.gate_proj.weight"] = torch.randn(f, d, generator=g) * d ** -0.5
+    W[lp + "mlp.up_proj.weight"] = torch.randn(f, d, generator=g) * d ** -0.5
+    W[lp + "mlp.down_proj.weight"] = torch.randn(d, f, generator=g) * f ** -0.5
+    W[lp + "input_layernorm.weight"] = torch.ones(d)
+    W[lp + "post_attention_layernorm.weight"] = torch.ones(d)
+    for k in W:
+        W[k].requires_grad_(True)
+    h = torch.randn(1, L, d, generator=g, requires_grad=True)
+    pos = torch.arange(L)[None]
+    cos, sin = O.rope_cos_sin(pos, t.head_dim, t.rope_theta)
+    allowed = O.causal_allowed(torch.ones(1, L, dtype=torch.long))
+
+    def lm_layer():
+        out = O.llama_layer(h, W, lp, t, cos, sin, allowed)
+        out.sum().backward()
+
+    vp = "vision_tower.vision_model.encoder.layers.0."
+    dv = v.hidden_size
+    VW = {}
+    for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+        VW[vp + f"self_attn.{n}.weight"] = torch.randn(dv, dv, generator=g) * dv ** -0.5
+        VW[vp + f"self_attn.{n}.bias"] = torch.zeros(dv)
+    VW[vp + "mlp.fc1.weight"] = torch.randn(v.intermediate_size, dv, generator=g) * dv ** -0.5
+    VW[vp + "mlp.fc1.bias"] = torch.zeros(v.intermediate_size)
+    VW[vp + "mlp.fc2.weight"] = torch.randn(dv, v.intermediate_size, generator=g) * v.intermediate_size ** -0.5
+    VW[vp + "mlp.fc2.bias"] = torch.zeros(dv)
+    for n in ("layer_norm1", "layer_norm2"):
+        VW[vp + n + ".weight"] = torch.ones(dv)
+        VW[vp + n + ".bias"] = torch.zeros(dv)
+    vh = torch.randn(1, v.num_patches + 1, dv, generator=g)
+
+    def vit_layer():
+        with torch.no_grad():
+            O.clip_layer(vh, VW, vp, v)
+
+    Wh = (torch.randn(t.vocab_size, d, generator=g) * d ** -0.5).requires_grad_(True)
+    x = torch.randn(1, L, d, generator=g, requires_grad=True)
+    tgt = torch.randint(0, t.vocab_size, (L,), generator=g)
+
+    def head():
+        logits = torch.nn.functional.linear(x, Wh)
+        torch.nn.functional.cross_entropy(logits.view(-1, t.vocab_size), tgt).backward()
+
+    def timed(fn, reps):
+        fn()  # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return (time.perf_counter() - t0) / reps
+
+    t_start = time.perf_counter()
+    t_lm = timed(lm_layer, 1)
+    reps = max(1, int((budget_s * 0.6) / max(t_lm, 1e-3)))
+    if reps > 1:
+        t_lm = timed(lm_layer, min(reps, 5))
+    t_vit = timed(vit_layer, 2)
+    t_head = timed(head, 1)
+    per_sample = t.num_hidden_layers * t_lm + O.needed_vision_layers(ocfg, -2) * t_vit + t_head
+    return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle fp32 on {threads} host threads: 1 Vicuna-7B decoder layer fwd+bwd "
+                       f"({t_lm:.2f}s) + 1 CLIP-L/14 layer fwd ({t_vit:.3f}s) + lm_head fwd+bwd ({t_head:.2f}s) at "
+                       f"B=1, L={L}, extrapolated x{t.num_hidden_layers} LM / x{O.needed_vision_layers(ocfg, -2)} "
+                       f"ViT layers; {time.perf_counter() - t_start:.1f}s of CPU work")}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from cullavo_amd import ops
+    from cullavo_amd.trainer import CuLLaVO_Trainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    opt = {"MODEL": {"CONFIG": args.config}, "LLM": {"TRAINABLE": args.trainable},
+           "DATA": {"BATCH_SIZE_PER_GPU": args.batch, "TEXT_LEN": args.text_len, "IMAGE_COL": 35,
+                    "STEPS": args.warmup + args.steps},
+           "BUCKET_MB": args.bucket_mb}
+    tr = CuLLaVO_Trainer(opt)
+    rank = tr.accel.process_index
+    tr.init_train()
+    cm = tr.model.cullavo_model
+    batch = next(iter(tr.train_dataloaders))  # resident in HBM before timing
+
+    def step():
+        with tr.accel.accumulate(tr.model):
+            info, _, _ = tr.train_step(batch)
+        return info["loss_llm"]
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+
+    # dominant kernel: the fused gate|up GEMM of the decoder layers, timed with HIP events on
+    # the stream it is launched on
+    cfg = cm.config
+    T = args.batch * (args.text_len + cfg.vision_config.num_patches - 1)
+    d, F_ = cfg.text_config.hidden_size, cfg.text_config.intermediate_size
+    ops.trace_gemm((T, 2 * F_, d, 0, 0))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms, kern_n = ops.trace_result()
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_v = float(loss)
+
+    from cullavo_amd.perf import flops_per_sample
+
+    fl = flops_per_sample(cfg, args.text_len, args.trainable)
+    samples = world * args.batch * args.steps
+    value = samples / elapsed
+    step_tflops = fl["train"] * world * args.batch / (elapsed / args.steps) / 1e12
+    gemm_flops = 2.0 * T * 2 * F_ * d
+    achieved = gemm_flops / (kern_ms * 1e-3) / 1e12 if kern_n else None
+    if rank == 0:
+        line = {
+            "metric": "train-step samples/sec (336px img + 512-tok prompt, 7B LM)",
+            "value": round(value, 4),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (seeded ids/pixels/labels in HBM, random-init weights)",
+            "config": {"workload": f"config 3: ViT-L/14-336 + Vicuna-7B, seq 576+512 (L={args.text_len + 575}), "
+                                   f"bs={args.batch}/GPU, bf16, {args.trainable} fine-tune (vision frozen), AdamW",
+                       "model": args.config, "global_batch": world * args.batch,
+                       "seq_len": args.text_len + cfg.vision_config.num_patches - 1,
+                       "parallelism": f"dp{world}", "trainable": args.trainable},
+            "model_tflops_per_gpu": round(step_tflops / world, 2),
+            "mfu": round(step_tflops / world / PEAK_BF16_TFLOPS, 4),
+            "loss": round(loss_v, 5),
+            "roofline": {
+                "kernel": f"gemm_k<0,0,bf16> gate|up projection M={T} N={2 * F_} K={d}",
+                "bound": "mfma",
+                "achieved": round(achieved, 2) if achieved else None,
+                "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+                "traffic": None,
+                "avg_ms": round(kern_ms, 4) if kern_n else None,
+                "launches_timed": kern_n,
+                "flops_per_launch": gemm_flops,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

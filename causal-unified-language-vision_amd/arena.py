@@ -40,6 +40,7 @@ class ParamArena:
         self.trainable = trainable
         self.grad_flat = None
         self._written: set[str] = set()
+        self._write_hooks: list = []  # called with the keys whose gradient write is enqueued
         if trainable:
             self.grad_flat = torch.zeros(off, dtype=dtype, device=self.device)
             self._attach_grads()
@@ -85,6 +86,12 @@ class ParamArena:
     def mark_written(self, keys: list[str]):
         self._written.update(keys)
 
+    def commit(self, keys: list[str]):
+        """The kernels writing these keys' gradients are enqueued on the current stream
+        (DP bucket hooks may now launch their all-reduce behind them)."""
+        for h in self._write_hooks:
+            h(keys)
+
     def zero_grad(self):
         """Start a new accumulation cycle. Buffers are not cleared: the first backward write
         uses beta = 0. Parameters that were never written last cycle are zeroed explicitly."""
@@ -107,6 +114,12 @@ class ParamArena:
 
 def grad_slot(p: nn.Parameter, span=None):
     return p._cv_arena.grad_slot(p._cv_key, span)
+
+
+def commit(*ps):
+    for p in ps:
+        if p is not None and p.requires_grad:
+            p._cv_arena.commit([p._cv_key])
 
 
 def trainable(p) -> bool:

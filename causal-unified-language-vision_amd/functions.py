@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
-from .arena import grad_slot, trainable
+from .arena import commit, grad_slot, trainable
 from .ops import ACT_GELU, ACT_QUICK_GELU
 
 
@@ -37,12 +37,14 @@ def _write_dw(dy, x, w):
     if trainable(w):
         g, beta = grad_slot(w)
         ops.linear_dw(dy, x, g, beta=beta)
+        commit(w)
 
 
 def _write_bias(dy, b):
     if trainable(b):
         g, beta = grad_slot(b)
         ops.colsum(dy, g, beta=beta)
+        commit(b)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -118,10 +120,12 @@ class LlamaLayerFn(torch.autograd.Function):
         if trainable(layer.mlp.gate_proj.weight):
             g, beta = layer.gu_grad_slot()
             ops.linear_dw(dgu, x2, g, beta=beta)
+            commit(layer.mlp.gate_proj.weight, layer.mlp.up_proj.weight)
         del dgu
         wpost = layer.post_attention_layernorm.weight
         dw_post, beta_post = grad_slot(wpost) if trainable(wpost) else (None, 0.0)
         dh2 = ops.rmsnorm_bwd(dx2, h2, wpost, rstd2, dres=dh3, dw=dw_post, beta=beta_post)
+        commit(wpost)
         del dx2
         # attention
         do = ops.linear_dx(dh2, layer.self_attn.o_proj.weight)
@@ -137,10 +141,13 @@ class LlamaLayerFn(torch.autograd.Function):
         if trainable(layer.self_attn.q_proj.weight):
             g, beta = layer.qkv_grad_slot()
             ops.linear_dw(dqkv, x1, g, beta=beta)
+            sa = layer.self_attn
+            commit(sa.q_proj.weight, sa.k_proj.weight, sa.v_proj.weight)
         del dqkv
         win = layer.input_layernorm.weight
         dw_in, beta_in = grad_slot(win) if trainable(win) else (None, 0.0)
         dh = ops.rmsnorm_bwd(dx1, h, win, rstd1, dres=dh2, dw=dw_in, beta=beta_in)
+        commit(win)
         return (dh, None, None) + (None,) * len(layer.fn_params())
 
 
@@ -186,6 +193,7 @@ class ClipLayerFn(torch.autograd.Function):
         ln2 = layer.layer_norm2
         dw2, db2, beta2 = _ln_slots(ln2)
         dh2 = ops.layernorm_bwd(dx2, h2, ln2.weight, m2, r2, dres=dh3, dw=dw2, db=db2, beta=beta2)
+        commit(ln2.weight, ln2.bias)
         do = ops.linear_dx(dh2, sa.out_proj.weight)
         _write_dw(dh2, o, sa.out_proj.weight)
         _write_bias(dh2, sa.out_proj.bias)
@@ -198,9 +206,12 @@ class ClipLayerFn(torch.autograd.Function):
             ops.linear_dw(dqkv, x1, g, beta=beta)
             gb, betab = layer.qkv_bias_grad_slot()
             ops.colsum(dqkv, gb, beta=betab)
+            commit(sa.q_proj.weight, sa.k_proj.weight, sa.v_proj.weight, sa.q_proj.bias, sa.k_proj.bias,
+                   sa.v_proj.bias)
         ln1 = layer.layer_norm1
         dw1, db1, beta1 = _ln_slots(ln1)
         dh = ops.layernorm_bwd(dx1, h, ln1.weight, m1, r1, dres=dh2, dw=dw1, db=db1, beta=beta1)
+        commit(ln1.weight, ln1.bias)
         return (dh, None, None, None) + (None,) * len(layer.fn_params())
 
 
@@ -259,6 +270,7 @@ class EmbeddingFn(torch.autograd.Function):
             if beta == 0.0:
                 g.zero_()
             ops.embedding_bwd(ctx.ids, dout.reshape(-1, w.shape[1]).contiguous(), g, beta=1.0)
+            commit(w)
         return None, None
 
 
@@ -315,4 +327,5 @@ class HeadLossFn(torch.autograd.Function):
         del dl
         dw, beta = grad_slot(norm_w) if trainable(norm_w) else (None, 0.0)
         dh = ops.rmsnorm_bwd(dx, h, norm_w, rstd, dw=dw, beta=beta) if ctx.needs_input_grad[0] else None
+        commit(norm_w)
         return (dh, None, None, None) + (None,) * len(lm.head_params())

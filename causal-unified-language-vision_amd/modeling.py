@@ -58,7 +58,7 @@ class _NormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from .arena import grad_slot, trainable
+        from .arena import commit, grad_slot, trainable
         x2, w, b, mean, rstd = ctx.saved
         dy2 = dy.reshape(x2.shape).contiguous()
         if ctx.kind == "rms":
@@ -72,6 +72,7 @@ class _NormFn(torch.autograd.Function):
                 dw = db = None
                 beta = 0.0
             dx = ops.layernorm_bwd(dy2, x2, w, mean, rstd, dw=dw, db=db, beta=beta)
+        commit(w, b)
         return dx.view(ctx.shp), None, None, None, None
 
 

@@ -51,12 +51,40 @@ def _ld(t: torch.Tensor) -> int:
 
 
 # ---- GEMM ------------------------------------------------------------------------------------
+_TRACE = {"key": None, "events": []}
+
+
+def trace_gemm(key):
+    """Time every launch whose (M, N, K, a_layout, b_layout) == key with HIP events recorded on
+    the stream the kernel is launched on (bench.py's roofline); key=None stops tracing."""
+    _TRACE["key"] = key
+    _TRACE["events"] = []
+
+
+def trace_result():
+    """(average ms per traced launch, number of launches); synchronises the events."""
+    evs = _TRACE["events"]
+    if not evs:
+        return 0.0, 0
+    evs[-1][1].synchronize()
+    ms = [a.elapsed_time(b) for a, b in evs]
+    _TRACE["key"] = None
+    return sum(ms) / len(ms), len(ms)
+
+
 def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
          alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
          beta: float = 0.0):
     _dev(A, B, C, bias, preact, residual)
+    traced = _TRACE["key"] is not None and _TRACE["key"] == (M, N, K, a_layout, b_layout)
+    if traced:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
     call("gemm", a_layout, b_layout, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _dt(C), float(alpha),
          _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _stream())
+    if traced:
+        e1.record(torch.cuda.current_stream())
+        _TRACE["events"].append((e0, e1))
     return C
 
 

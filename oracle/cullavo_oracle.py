@@ -428,30 +428,3 @@ def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, la
     loss = shifted_ce(logits, labels, mask)
     return loss, logits, {"attention_mask": mask, "position_ids": pos, "image_features": image_features,
                           "inputs_embeds": embeds, "hidden": hidden}
-
-
-# ---------------------------------------------------------------------------------------------
-# algorithmic work used by bench.py's roofline
-# ---------------------------------------------------------------------------------------------
-def flops_per_sample(cfg: CuLLaVOCfg, text_len: int, trainable: str = "full") -> dict[str, float]:
-    """Forward FLOPs per sample and train-step FLOPs actually executed by our step."""
-    v, t = cfg.vision, cfg.text
-    T = v.num_patches + 1
-    L = text_len + v.num_patches - 1
-    nv = needed_vision_layers(cfg, cfg.vision_feature_layer)
-    dv = v.hidden_size
-    vit_layer = 2 * T * (4 * dv * dv + 2 * dv * v.intermediate_size) + 4 * T * T * dv
-    vit = nv * vit_layer + 2 * v.num_patches * dv * v.num_channels * v.patch_size ** 2
-    d, f = t.hidden_size, t.intermediate_size
-    proj = 2 * v.num_patches * (dv * d + d * d)
-    gemm_layer = 2 * L * (4 * d * d + 3 * d * f)
-    attn_layer = 2 * L * L * d  # causal: half of the 4*L^2*d of QK^T + PV
-    head = 2 * L * d * t.vocab_size
-    lm_fwd = t.num_hidden_layers * (gemm_layer + attn_layer)
-    fwd = vit + proj + lm_fwd + head
-    if trainable == "full":  # LM + projector + head: dX and dW; vision frozen
-        bwd = t.num_hidden_layers * (2 * gemm_layer + 2.5 * attn_layer) + 2 * head + 2 * proj
-    else:  # frozen base: dX through the LM, dW only for projector / head / embedding
-        bwd = t.num_hidden_layers * (gemm_layer + 2.5 * attn_layer) + 2 * head + 2 * proj
-    return {"fwd": float(fwd), "train": float(fwd + bwd), "lm_gemm_layer": float(gemm_layer),
-            "lm_attn_layer": float(attn_layer), "vit": float(vit), "head": float(head), "proj": float(proj)}
