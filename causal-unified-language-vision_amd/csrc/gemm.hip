@@ -118,6 +118,61 @@ DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// epilogue for one lane's C[m][n .. n+3] (bias -> preact -> act -> residual -> beta -> store)
+template <int CT>
+DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
+  if (m >= p.M || n >= p.N) return;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = acc[j] * p.alpha;
+  if (p.bias) {
+    const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += bf2f(bv[j]);
+  }
+  if (p.act != CULLAVO_ACT_NONE || p.preact) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);
+    if (p.preact) {
+      u16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+      *reinterpret_cast<u16x4*>(p.preact + m * p.ldc + n) = o;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = act_apply(p.act, v[j]);
+  }
+  if (p.residual) {
+    const u16x4 rv = *reinterpret_cast<const u16x4*>(p.residual + m * p.ldr + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
+  }
+  if (CT == CULLAVO_DT_BF16) {
+    u16* cp = (u16*)p.C + m * p.ldc + n;
+    if (p.beta != 0.f) {
+      const u16x4 old = *reinterpret_cast<const u16x4*>(cp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += p.beta * bf2f(old[j]);
+    }
+    u16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+    *reinterpret_cast<u16x4*>(cp) = o;
+  } else {
+    float* cp = (float*)p.C + m * p.ldc + n;
+    f32x4 o;
+    if (p.beta != 0.f) {
+      const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = v[j] + p.beta * old[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = v[j];
+    }
+    *reinterpret_cast<f32x4*>(cp) = o;
+  }
+}
+
 template <int AL, int BL, int CT>
 __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -184,60 +239,213 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
 #pragma unroll
   for (int tm = 0; tm < 4; ++tm) {
     const int64_t m = m0 + wm * 64 + tm * 16 + (lane & 15);
-    if (m >= p.M) continue;
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) {
       const int64_t n = n0 + wn * 64 + tn * 16 + (lane >> 4) * 4;
-      if (n >= p.N) continue;
-      float v[4];
+      store4<CT>(p, acc[tm][tn], m, n);
+    }
+  }
+}
+
+// ============================================================================================
+// 256-row tile, 8 waves, operands streamed by LDS-DMA (buffer_load ... lds)
+// ============================================================================================
+// Every 1 KiB LDS-DMA wave-instruction writes lane-linearly, so the XOR-swizzled LDS images
+// above are produced by permuting each lane's SOURCE address (cdna_hip_programming.md rule
+// 21). Out-of-range rows / K tails are zero-filled by the buffer range check: such lanes get
+// an offset past num_records.
+constexpr unsigned kOOB = 0x7FFFFFF0u;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const u16* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+
+// fill one [ROWS][64] (layout 0) or [64][ROWS] (layout 1) operand image; NW waves share it
+template <int LAYOUT, int ROWS, int NW>
+DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
+                  char* lds, int wave, int lane) {
+  if (LAYOUT == 0) {
+    constexpr int kPieces = ROWS / 8;  // 8 rows of 128 B per 1 KiB piece
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[tm][tn][j] * p.alpha;
-      if (p.bias) {
-        const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
+    for (int i = 0; i < kPieces / NW; ++i) {
+      const int pc = wave + NW * i;
+      const int row = pc * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
+      const unsigned off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
+    }
+  } else {
+    constexpr int RB = ROWS * 2;            // bytes per k-row of the image
+    constexpr int kPieces = 64 * RB / 1024;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += bf2f(bv[j]);
+    for (int i = 0; i < kPieces / NW; ++i) {
+      const int pc = wave + NW * i;
+      const int byte = pc * 1024 + lane * 16;
+      const int k = byte / RB, b = byte % RB;
+      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+      const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
+      const unsigned off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
+    }
+  }
+}
+
+template <int ROWS>
+DEV int img1w_off(int k, int unit) { return k * (ROWS * 2) + ((unit ^ swz1(k)) << 5); }
+
+// Transposed fragment reads issued by inline asm. The ds_read_tr16 builtin carries no
+// memory-operand info, so hipcc (ROCm 7.2) assumes it may alias the in-flight LDS-DMA of the
+// next stage and waits vmcnt(0) before it, serialising the prefetch (measured: the (0,1)
+// and (1,1) kernels lost 25-45 % to it). The asm reads are invisible to the compiler's
+// counters: tr_issue() only issues, tr_wait() (ONE s_waitcnt lgkmcnt(0) that ties the
+// destination registers) must run before any consumer (cdna_hip_programming.md §5.7 item 1,
+// form (ii) + rule 18's sched_barrier). Older compiler-issued LDS reads are also retired by
+// that wait, and extra younger asm reads only make the compiler's own counted waits stricter.
+DEV unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
+
+template <int ROWS>
+DEV void tr_issue(const char* lds, int rbase, int ks, int lane, s16x4& lo, s16x4& hi) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int unit = rbase >> 4;
+  const int k1 = ks * 32 + 8 * g + q;
+  const unsigned a0 = lds_addr(lds + img1w_off<ROWS>(k1, unit) + 8 * p);
+  const unsigned a1 = lds_addr(lds + img1w_off<ROWS>(k1 + 4, unit) + 8 * p);
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
+               : "=&v"(lo), "=&v"(hi)
+               : "v"(a0), "v"(a1)
+               : "memory");
+}
+
+DEV frag8 tr_join(const s16x4& lo, const s16x4& hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(frag8, v);
+}
+
+// wait for every outstanding LDS read and tie up to 4 fragment pairs (rule 18 fence after)
+DEV void tr_wait4(s16x4& a, s16x4& b, s16x4& c, s16x4& d, s16x4& e, s16x4& f, s16x4& g, s16x4& h) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
+               :: "memory");
+}
+
+template <int N>
+DEV void tie_all(s16x4 (&lo)[N], s16x4 (&hi)[N]) {
+  s16x4 d0 = {}, d1 = {}, d2 = {}, d3 = {}, d4 = {}, d5 = {};
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    if (i + 3 < N) tr_wait4(lo[i], hi[i], lo[i + 1], hi[i + 1], lo[i + 2], hi[i + 2], lo[i + 3], hi[i + 3]);
+    else if (i + 1 < N) tr_wait4(lo[i], hi[i], lo[i + 1], hi[i + 1], d0, d1, d2, d3);
+    else tr_wait4(lo[i], hi[i], d0, d1, d2, d3, d4, d5);
+  }
+}
+
+// fragment X[idx = rbase + (lane&15)][k = ks*32 + 8*(lane>>4) + j] from a ROWS-wide image
+template <int LAYOUT, int ROWS>
+DEV frag8 read_frag_w(const char* lds, int rbase, int ks, int lane) {
+  if (LAYOUT == 0) return read_frag<0>(lds, rbase, ks, lane);
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int unit = rbase >> 4;
+  const int k1 = ks * 32 + 8 * g + q;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1w_off<ROWS>(k1, unit) + 8 * p));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1w_off<ROWS>(k1 + 4, unit) + 8 * p));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(frag8, v);
+}
+
+template <int AL, int BL, int CT, int BMT, int BN>
+__global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
+  constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
+  constexpr int TILE_A = BM2 * BK * 2;
+  constexpr int TILE_B = BN * BK * 2;
+  constexpr int STAGE = TILE_A + TILE_B;
+  constexpr int WN_COLS = BN / 4;     // per-wave N extent (4 waves across N)
+  constexpr int TN = WN_COLS / 16;    // 16-col MFMA tiles per wave
+  constexpr int TMW = BM2 / 32;       // 16-row MFMA tiles per wave (BM/2 rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * p.tiles_n;
+  const int group = lid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  const int tm_idx = first_m + (lid % per_group) % gsize;
+  const int tn_idx = (lid % per_group) / gsize;
+  const int64_t m0 = (int64_t)tm_idx * BM2, n0 = (int64_t)tn_idx * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  f32x4 acc[TMW][TN];
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)cdiv(p.K, BK);
+  dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, 0, p.K, smem, wave, lane);
+  dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, 0, p.K, smem + TILE_A, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE;
+      const int64_t k1 = (int64_t)(kt + 1) * BK;
+      dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, k1, p.K, nxt, wave, lane);
+      dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      frag8 fb[TN];
+      s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
+      if constexpr (BL == 1) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t) tr_issue<BN>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane, blo[t], bhi[t]);
       }
-      if (p.act != CULLAVO_ACT_NONE || p.preact) {
+      if constexpr (AL == 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);
-        if (p.preact) {
-          u16x4 o;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-          *reinterpret_cast<u16x4*>(p.preact + m * p.ldc + n) = o;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_apply(p.act, v[j]);
+        for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * (BM2 / 2) + tm * 16, ks, lane, alo[tm], ahi[tm]);
       }
-      if (p.residual) {
-        const u16x4 rv = *reinterpret_cast<const u16x4*>(p.residual + m * p.ldr + n);
+      if constexpr (BL == 1) tie_all<TN>(blo, bhi);
+      if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
+      if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
+      for (int t = 0; t < TN; ++t)
+        fb[t] = BL == 1 ? tr_join(blo[t], bhi[t]) : read_frag<0>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane);
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm) {
+        const frag8 fa = AL == 1 ? tr_join(alo[tm], ahi[tm]) : read_frag<0>(cur, wm * (BM2 / 2) + tm * 16, ks, lane);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
       }
-      if (CT == CULLAVO_DT_BF16) {
-        u16* cp = (u16*)p.C + m * p.ldc + n;
-        if (p.beta != 0.f) {
-          const u16x4 old = *reinterpret_cast<const u16x4*>(cp);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] += p.beta * bf2f(old[j]);
-        }
-        u16x4 o;
+  for (int tm = 0; tm < TMW; ++tm) {
+    const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-        *reinterpret_cast<u16x4*>(cp) = o;
-      } else {
-        float* cp = (float*)p.C + m * p.ldc + n;
-        f32x4 o;
-        if (p.beta != 0.f) {
-          const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = v[j] + p.beta * old[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = v[j];
-        }
-        *reinterpret_cast<f32x4*>(cp) = o;
-      }
+    for (int tn = 0; tn < TN; ++tn) {
+      const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
+      store4<CT>(p, acc[tm][tn], m, n);
     }
   }
 }
@@ -254,7 +462,57 @@ int launch(const GemmArgs& p, hipStream_t s) {
   return cullavo_check_launch("gemm");
 }
 
+template <int AL, int BL, int CT, int BM2, int BN2>
+int launch256(GemmArgs p, hipStream_t s) {
+  const int smem = 2 * (BM2 * BK * 2 + BN2 * BK * 2);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, BM2);
+  p.tiles_n = (int)cdiv(p.N, BN2);
+  gemm256_k<AL, BL, CT, BM2, BN2><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemm256");
+}
+
+// Kernel-shape choice. Time model = FLOPs / (per-tile rate of the shape) x (whole rounds of
+// tiles over the 256 CUs / exact rounds): the 8-wave kernels run one 512-thread block per CU,
+// so a grid of 544 tiles takes 3 rounds for 2.125 rounds of work. Per-tile rates (TFLOP/s,
+// measured on MI355X with tools/gemm_bench.py): 256x256 ~1250, 192x256
+// ~1190 (A K-contiguous only), 128x128 4-wave (2 blocks/CU, 512 slots) ~840.
+enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3 };
+int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
+  if (force >= 0) return force;
+  struct C { int id; int64_t bm, bn, slots; double rate; };
+  const C cands[3] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, 1250.0},
+                      {kT192x256, 192, 256, 256, 1190.0}};
+  double best = 1e300;
+  int bid = kT128;
+  for (const C& c : cands) {
+    if (c.id == kT192x256 && a_layout != 0) continue;
+    const int64_t tiles = cdiv(M, c.bm) * cdiv(N, c.bn);
+    const double exact = (double)tiles / (double)c.slots;
+    const double rounds = (double)cdiv(tiles, c.slots);
+    // padded work of partial edge tiles is paid too
+    const double eff_area = (double)(M * N) / (double)(tiles * c.bm * c.bn);
+    const double t = (rounds / exact) / (c.rate * eff_area);
+    if (t < best * 0.999) { best = t; bid = c.id; }
+  }
+  (void)K;
+  return bid;
+}
+
 }  // namespace
+
+static int g_force_tile = -1;
+
+extern "C" int cullavo_gemm_set_tile(int mode) {
+  const int prev = g_force_tile;
+  g_force_tile = (mode >= 0 && mode <= 3) ? mode : -1;
+  return prev;
+}
 
 extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K, const void* A,
                             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
@@ -284,6 +542,22 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
   p.tiles_m = (int)tm; p.tiles_n = (int)tn;
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
+  const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
+  const int64_t b_ext = b_layout == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N;
+  const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
+  int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
+  if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  if (tile != kT128) {
+#define L256(AL, BL)                                                                                         \
+  if (tile == kT256x256) return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256>(p, s); \
+  if (tile == kT192x256 && AL == 0) return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256>(p, s); \
+  return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 128>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 128>(p, s);
+    if (a_layout == 0 && b_layout == 0) { L256(0, 0) }
+    if (a_layout == 0 && b_layout == 1) { L256(0, 1) }
+    if (a_layout == 1 && b_layout == 0) { L256(1, 0) }
+    L256(1, 1)
+#undef L256
+  }
   if (a_layout == 0 && b_layout == 0) return f32 ? launch<0, 0, CULLAVO_DT_F32>(p, s) : launch<0, 0, CULLAVO_DT_BF16>(p, s);
   if (a_layout == 0 && b_layout == 1) return f32 ? launch<0, 1, CULLAVO_DT_F32>(p, s) : launch<0, 1, CULLAVO_DT_BF16>(p, s);
   if (a_layout == 1 && b_layout == 0) return f32 ? launch<1, 0, CULLAVO_DT_F32>(p, s) : launch<1, 0, CULLAVO_DT_BF16>(p, s);

@@ -243,15 +243,23 @@ __global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy,
 }
 
 // partial [nslots, cols] f32 -> out[c] = beta*out[c] + sum_p part[p][c]
+// block = 64 columns x 4 slot groups (coalesced 256 B row segments), fixed summation order
 template <typename TO>
 __global__ __launch_bounds__(256) void reduce_partials_k(const float* __restrict__ part, int nslots,
                                                          int cols, TO* __restrict__ out, float beta) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= cols) return;
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int p = 0; p < nslots; ++p) s += part[(int64_t)p * cols + col];
-  if (beta != 0.f) s += beta * Elt<TO>::ld(out, col);
-  Elt<TO>::st(out, col, s);
+  if (col < cols)
+    for (int p = g; p < nslots; p += 4) s += part[(int64_t)p * cols + col];
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < cols) {
+    s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    if (beta != 0.f) s += beta * Elt<TO>::ld(out, col);
+    Elt<TO>::st(out, col, s);
+  }
 }
 
 int nch_for(int64_t cols) {
@@ -273,7 +281,7 @@ int nch_for(int64_t cols) {
 
 template <typename TO>
 void launch_reduce(const float* part, int nslots, int cols, void* out, float beta, hipStream_t s) {
-  reduce_partials_k<TO><<<cdiv(cols, 256), 256, 0, s>>>(part, nslots, cols, (TO*)out, beta);
+  reduce_partials_k<TO><<<cdiv(cols, 64), 256, 0, s>>>(part, nslots, cols, (TO*)out, beta);
 }
 
 int bwd_blocks(int64_t rows) { return (int)std::min<int64_t>(kBwdBlocks, cdiv(rows, kRowsPerBlock)); }

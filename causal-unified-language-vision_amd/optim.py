@@ -20,7 +20,10 @@ class FusedAdamW(torch.optim.Optimizer):
     """torch.optim.Optimizer subclass (so torch LR schedulers drive param_groups[0]['lr'])."""
 
     def __init__(self, arenas: list[ParamArena], lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, state_dtype=torch.float32):
+                 weight_decay: float = 0.0, state_dtype=torch.bfloat16):
+        # state dtype defaults to the parameter dtype, as torch.optim.AdamW does for the
+        # reference's bf16-cast parameters (reference cullavo/load_cullavo.py:123-126);
+        # pass torch.float32 for f32 moments
         self.arenas = [a for a in arenas if a.trainable]
         params = [p for a in self.arenas for p in a.params.values()]
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))

@@ -64,6 +64,12 @@ int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
                  const void* bias, int act, void* preact,
                  const void* residual, int64_t ldr, float beta, void* stream);
 
+/* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
+ * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
+ * staged; 3 falls back to 2 when A is not K-contiguous). Returns the previous
+ * mode. For tests and tuning; not thread-safe. */
+int cullavo_gemm_set_tile(int mode);
+
 /* ---- norms -------------------------------------------------------------------------------
  * LlamaRMSNorm (tf:llama/modeling_llama.py:53-70): fp32 statistics, y = w * bf16(x*rstd).
  * rstd: [rows] f32 saved for backward. cols % 8 == 0, cols <= 8192. */

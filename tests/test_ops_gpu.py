@@ -43,9 +43,17 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.fixture(params=[0, 1, 2, 3, -1], ids=["t128", "t256x128", "t256x256", "t192x256", "auto"])
+def tile_mode(request):
+    from cullavo_amd import _lib
+    prev = _lib.lib().cullavo_gemm_set_tile(request.param)
+    yield request.param
+    _lib.lib().cullavo_gemm_set_tile(prev)
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES + [(520, 264, 8704), (8, 1032, 136)])
 @pytest.mark.parametrize("al,bl", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_layouts(M, N, K, al, bl):
+def test_gemm_layouts(M, N, K, al, bl, tile_mode):
     if al == 1 and M % 8:
         pytest.skip("a_layout 1 needs M % 8 == 0")
     A = rnd((M, K), 1)
@@ -59,7 +67,7 @@ def test_gemm_layouts(M, N, K, al, bl):
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
-def test_gemm_epilogues(act):
+def test_gemm_epilogues(act, tile_mode):
     M, N, K = 300, 264, 192
     x, w, b = rnd((M, K), 3), rnd((N, K), 4, 0.1), rnd((N,), 5, 0.1)
     r = rnd((M, N), 6)
@@ -70,7 +78,7 @@ def test_gemm_epilogues(act):
     close(y, a.to(BF).float() + r.float(), 8e-3, "epilogue")
 
 
-def test_gemm_f32_accumulate_beta():
+def test_gemm_f32_accumulate_beta(tile_mode):
     M, N, K = 128, 192, 256
     dy, x = rnd((M, N), 7), rnd((M, K), 8)
     out = rnd((N, K), 9, dtype=torch.float32).to(DEV)
@@ -80,7 +88,7 @@ def test_gemm_f32_accumulate_beta():
     close(out, ref, 1e-5, "dw beta f32")
 
 
-def test_linear_dx_dw_bf16():
+def test_linear_dx_dw_bf16(tile_mode):
     M, N, K = 520, 384, 264
     dy, w, x = rnd((M, N), 10), rnd((N, K), 11), rnd((M, K), 12)
     dx = ops().linear_dx(dy.to(DEV), w.to(DEV))
@@ -90,7 +98,7 @@ def test_linear_dx_dw_bf16():
     close(dw, dy.float().T @ x.float(), 8e-3, "dw")
 
 
-def test_gemm_strided_operands():
+def test_gemm_strided_operands(tile_mode):
     # q|k|v fused projection output consumed as strided views (ld > K)
     M, K, N = 96, 128, 64
     big = rnd((M, 3 * K), 13)
