@@ -56,7 +56,8 @@ class GradReducer:
 
     def _add_bucket(self, ai, ar, keys):
         lo, hi = ar.slice_of(keys)
-        b = {"arena": ai, "keys": set(keys), "lo": lo, "hi": hi, "pending": set(keys), "work": None}
+        b = {"arena": ai, "keys": set(keys), "lo": lo, "hi": hi, "pending": set(keys), "work": None,
+             "launched": False}
         for k in keys:
             self._key_bucket[(ai, k)] = len(self.buckets)
         self.buckets.append(b)
@@ -65,6 +66,7 @@ class GradReducer:
         for b in self.buckets:
             b["pending"] = set(b["keys"])
             b["work"] = None
+            b["launched"] = False
         self.launched = []
 
     def _on_write(self, ai):
@@ -77,12 +79,13 @@ class GradReducer:
                     continue
                 b = self.buckets[bi]
                 b["pending"].discard(k)
-                if not b["pending"] and b["work"] is None:
+                if not b["pending"] and not b["launched"]:
                     self._launch(bi)
         return hook
 
     def _launch(self, bi):
         b = self.buckets[bi]
+        b["launched"] = True
         ar = self.arenas[b["arena"]]
         view = ar.grad_flat[b["lo"]:b["hi"]]
         if self.stream is not None:
@@ -108,7 +111,7 @@ class GradReducer:
         if not self.enabled:
             return
         for bi, b in enumerate(self.buckets):
-            if b["work"] is None:
+            if not b["launched"]:
                 self._launch(bi)
         if self.stream is not None:
             with torch.cuda.stream(self.stream):
