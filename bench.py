@@ -122,6 +122,30 @@ def cpu_baseline(cfg, text_len: int, budget_s: float):
                        f"ViT layers; {time.perf_counter() - t_start:.1f}s of CPU work")}
 
 
+def gemm_kernel_name(M, N, K):
+    """rocprof name + workgroup count of the kernel cullavo_gemm picks for a (0,0) problem"""
+    import ctypes
+    from cullavo_amd import _lib
+    g = ctypes.c_int64(0)
+    tile = _lib.lib().cullavo_gemm_plan(M, N, K, 0, 0, ctypes.byref(g))
+    names = {0: "gemm_k<0, 0, 1>", 1: "gemm256_k<0, 0, 1, 256, 128>", 2: "gemm256_k<0, 0, 1, 256, 256>",
+             3: "gemm256_k<0, 0, 1, 192, 256>"}
+    return names[tile], int(g.value)
+
+
+def measured_traffic(kname, grid):
+    """HBM bytes per launch of the roofline kernel from the committed PMC pass (None if the
+    profile was taken on a different kernel shape)."""
+    path = os.path.join(REPO, "profiles", "roofline_traffic.json")
+    try:
+        rec = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if rec.get("kernel") == kname and int(rec.get("grid", -1)) == grid:
+        return rec.get("bytes_per_launch")
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -183,6 +207,8 @@ def main():
     value = samples / elapsed
     step_tflops = fl["train"] * world * args.batch / (elapsed / args.steps) / 1e12
     gemm_flops = 2.0 * T * 2 * F_ * d
+    kname, grid = gemm_kernel_name(T, 2 * F_, d)
+    traffic = measured_traffic(kname, grid)
     achieved = gemm_flops / (kern_ms * 1e-3) / 1e12 if kern_n else None
     if rank == 0:
         line = {
@@ -207,13 +233,15 @@ def main():
             "mfu": round(step_tflops / world / PEAK_BF16_TFLOPS, 4),
             "loss": round(loss_v, 5),
             "roofline": {
-                "kernel": f"gemm_k<0,0,bf16> gate|up projection M={T} N={2 * F_} K={d}",
+                "kernel": f"{kname} grid={grid}: fused gate|up projection M={T} N={2 * F_} K={d}",
                 "bound": "mfma",
                 "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; "
+                                "profiles/roofline_traffic.json)" if traffic else None,
                 "avg_ms": round(kern_ms, 4) if kern_n else None,
                 "launches_timed": kern_n,
                 "flops_per_launch": gemm_flops,

@@ -514,6 +514,15 @@ extern "C" int cullavo_gemm_set_tile(int mode) {
   return prev;
 }
 
+extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid) {
+  int tile = choose_tile(M, N, K, a_layout, g_force_tile);
+  if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  static const int bm[4] = {128, 256, 256, 192}, bn[4] = {128, 128, 256, 256};
+  if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
+  (void)b_layout;
+  return tile;
+}
+
 extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K, const void* A,
                             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
                             float alpha, const void* bias, int act, void* preact, const void* residual,

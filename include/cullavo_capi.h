@@ -69,6 +69,9 @@ int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
  * staged; 3 falls back to 2 when A is not K-contiguous). Returns the previous
  * mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
+/* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
+ * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls. */
+int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid);
 
 /* ---- norms -------------------------------------------------------------------------------
  * LlamaRMSNorm (tf:llama/modeling_llama.py:53-70): fp32 statistics, y = w * bf16(x*rstd).
