@@ -450,6 +450,278 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   }
 }
 
+// ============================================================================================
+// 256x256 ping-pong kernel: 8 phases per 2 K-tiles, LDS-DMA kept in flight across barriers
+// ============================================================================================
+// LDS (128 KiB): 2 buffers x 4 half-tiles of [128 local rows][64 k] (or [64 k][128]):
+//   A0 = tile rows {0-63, 128-191}   (the m-half 0 rows of wave rows 0 and 1)
+//   A1 = tile rows {64-127, 192-255}
+//   B0 = tile cols {wc*64 + 0..31}, B1 = tile cols {wc*64 + 32..63} for wave cols wc = 0..3
+// Wave (wr, wc) owns output rows wr*128.., cols wc*64..; a K-tile is 4 phases, one C-quadrant
+// (4 m-tiles x 2 n-tiles x K=64 = 16 MFMAs) each:
+//   q0: read B0 sub + A(mh0) sub -> quadrant (mh0, nh0)
+//   q1: read B1 sub               -> (mh0, nh1)
+//   q2: read A(mh1) sub           -> (mh1, nh1)
+//   q3: (no read, B0 kept)        -> (mh1, nh0)
+// so a K-tile's half-tiles are last read at q0 (A0, B0), q1 (B1) and q2 (A1). Every phase stages
+// one half-tile of a later K-tile: q0 -> B1(j+1), q1 -> A1(j+1), q2 -> A0(j+2), q3 -> B0(j+2),
+// each >= 2 phases after the last read of the buffer slot it overwrites (WAR across the two
+// staggered wave groups), and a phase's wait vmcnt(8) (2 DMA instructions per half-tile per
+// wave, 4 half-tiles in flight) retires exactly what the NEXT phase reads (RAW: wait before the
+// phase's first barrier, read one phase later). Waves 4-7 run one barrier behind waves 0-3:
+// each SIMD alternates one wave's LDS reads + DMA issue with the other wave's MFMAs
+// (cdna_hip_programming.md "Pipelining across barriers", §5.5 T3+T4, T5 setprio).
+constexpr int kHalf = 16384;
+
+template <int LAYOUT, int SPL>
+DEV void dma_half(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0,
+                  int64_t K, char* lds, int h, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pc = wave + 8 * i;  // 16 x 1 KiB pieces per half-tile
+    int lr, k;
+    if (LAYOUT == 0) {
+      lr = pc * 8 + (lane >> 3);
+      k = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
+    } else {
+      const int byte = pc * 1024 + lane * 16;
+      k = byte >> 8;
+      const int b = byte & 255;
+      lr = (((b >> 5) ^ swz1(k)) << 4) + ((b >> 4) & 1) * 8;
+    }
+    const int64_t gi = idx0 + (lr / SPL) * (2 * SPL) + h * SPL + (lr % SPL), gk = k0 + k;
+    unsigned off;
+    if (LAYOUT == 0) off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
+    else off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
+  }
+}
+
+// Loop-invariant part of a half-tile piece's per-lane source offset (K-tile 0, no K-tail
+// check): the K advance goes into the scalar soffset, so the DMA issue in the phase's load
+// segment is two buffer_load ... lds and no per-lane address arithmetic. Out-of-range rows get
+// kOOBv, which stays past num_records with or without the soffset added.
+constexpr unsigned kOOBv = 0x80000000u;
+
+template <int LAYOUT, int SPL>
+DEV unsigned dma_voff(int64_t ld, int64_t idx0, int64_t idx_max, int h, int pc, int lane) {
+  int lr, k;
+  if (LAYOUT == 0) {
+    lr = pc * 8 + (lane >> 3);
+    k = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
+  } else {
+    const int byte = pc * 1024 + lane * 16;
+    k = byte >> 8;
+    const int b = byte & 255;
+    lr = (((b >> 5) ^ swz1(k)) << 4) + ((b >> 4) & 1) * 8;
+  }
+  const int64_t gi = idx0 + (lr / SPL) * (2 * SPL) + h * SPL + (lr % SPL);
+  if (gi >= idx_max) return kOOBv;
+  return LAYOUT == 0 ? (unsigned)((gi * ld + k) * 2) : (unsigned)(((int64_t)k * ld + gi) * 2);
+}
+
+// 16 x 8 fragment of a half-tile (local rows rbase + lane&15, k = ks*32 + 8*(lane>>4) + j)
+struct HFrag {
+  s16x4 lo, hi;
+};
+
+template <int LAYOUT>
+DEV void hfrag_issue(const char* lds, int rbase, int ks, int lane, HFrag& f) {
+  if (LAYOUT == 0) {
+    const int row = rbase + (lane & 15);
+    const unsigned a = lds_addr(lds + img0_off(row, ks * 4 + (lane >> 4)));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    f.lo = __builtin_shufflevector(v, v, 0, 1, 2, 3);
+    f.hi = __builtin_shufflevector(v, v, 4, 5, 6, 7);
+  } else {
+    tr_issue<128>(lds, rbase, ks, lane, f.lo, f.hi);
+  }
+}
+
+template <int N>
+DEV void hfrag_tie(HFrag (&f)[N]) {
+  static_assert(N == 4 || N == 8, "tie size");
+#pragma unroll
+  for (int i = 0; i < N; i += 4)
+    tr_wait4(f[i].lo, f[i].hi, f[i + 1].lo, f[i + 1].hi, f[i + 2].lo, f[i + 2].hi, f[i + 3].lo, f[i + 3].hi);
+}
+
+DEV frag8 hfrag_val(const HFrag& f) { return tr_join(f.lo, f.hi); }
+
+// wait until at most n (uniform, in half-tiles) of this wave's LDS-DMA half-tiles are in flight
+DEV void wait_halves(int n) {
+  if (n >= 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n == 5) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if (n == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// S = half-tile slots in LDS (8: 128 KiB, 10: 160 KiB). Half-tiles are issued in the order
+// u = 4j + s (s: 0 A0, 1 B0, 2 B1, 3 A1) into slot u % S, half-tile u during phase u - C
+// (phases 1-indexed, phase 4j+q+1 computes quadrant q of K-tile j), C = S - 3. Then
+//   RAW: the reads of u happen >= C - 1 phases after its issue, H = S - 4 newer half-tiles may
+//        stay in flight at the wait one phase before (vmcnt(2H));
+//   WAR: u + S reuses slot u % S at phase u + S - C = u + 3 >= last read of u (<= u + 1) + 2.
+template <int AL, int BL, int CT, int S>
+__global__ __launch_bounds__(512, 1) void gemm8p_k(GemmArgs p) {
+  static_assert(S == 8 || S == 10, "slot count");
+  constexpr int C = S - 3;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * p.tiles_n;
+  const int group = lid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  const int tm_idx = first_m + (lid % per_group) % gsize;
+  const int tn_idx = (lid % per_group) / gsize;
+  const int64_t m0 = (int64_t)tm_idx * 256, n0 = (int64_t)tn_idx * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)cdiv(p.K, 64);
+  const int last_u = 4 * nk - 1;
+  auto slot = [&](int u) { return smem + (u % S) * kHalf; };
+  // per-lane source offsets of this wave's 2 pieces of each half-tile kind (A0, A1, B0, B1)
+  unsigned vo[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    vo[0][i] = dma_voff<AL, 64>(p.lda, m0, p.M, 0, wave + 8 * i, lane);
+    vo[1][i] = dma_voff<AL, 64>(p.lda, m0, p.M, 1, wave + 8 * i, lane);
+    vo[2][i] = dma_voff<BL, 32>(p.ldb, n0, p.N, 0, wave + 8 * i, lane);
+    vo[3][i] = dma_voff<BL, 32>(p.ldb, n0, p.N, 1, wave + 8 * i, lane);
+  }
+  const bool ktail = (p.K & 63) != 0;
+  auto stage = [&](int u) {
+    const int j = u >> 2, s = u & 3;
+    if (j >= nk) return;
+    char* dst = slot(u);
+    const int64_t k0 = (int64_t)j * 64;
+    const bool isA = s == 0 || s == 3;
+    const int h = isA ? (s == 3) : s - 1;
+    if (ktail && j == nk - 1) {  // zero-fill past K: full per-lane check
+      if (isA) dma_half<AL, 64>(ra, p.lda, m0, p.M, k0, p.K, dst, h, wave, lane);
+      else dma_half<BL, 32>(rb, p.ldb, n0, p.N, k0, p.K, dst, h, wave, lane);
+      return;
+    }
+    const int kind = isA ? h : 2 + h;
+    const int lay = isA ? AL : BL;
+    const int64_t ld = isA ? p.lda : p.ldb;
+    const int soff = (int)(lay == 0 ? k0 * 2 : k0 * ld * 2);
+    const __amdgpu_buffer_rsrc_t r = isA ? ra : rb;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const unsigned v = kind == 0 ? vo[0][i] : kind == 1 ? vo[1][i] : kind == 2 ? vo[2][i] : vo[3][i];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + (wave + 8 * i) * 1024), 16, v, soff, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int u = 0; u <= C; ++u) stage(u);
+  wait_halves(min(C, last_u) - 1);  // A0, B0 of K-tile 0 landed
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  HFrag fa[8], fb0[4], fb1[4];  // fa: 4 m-tiles x 2 ks of one m-half; fb*: 2 n-tiles x 2 ks
+
+  for (int j = 0; j < nk; ++j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mh = q >> 1, nh = (q == 1 || q == 2) ? 1 : 0;
+      const int ub = 4 * j;
+      // DMA first: issued behind a burst of ds_reads an LDS-DMA costs 100-185 cycles of issue
+      // (MI355X_MICROARCH.md cycle constants). Its slot (u_issue % S) is never one this phase
+      // reads (u_issue - u_read is 5..6 for S = 8, 7..8 for S = 10).
+      const int u_issue = ub + q + 1 + C;
+      stage(u_issue);
+      if (q == 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) hfrag_issue<BL>(slot(ub + 1), wc * 32 + (t >> 1) * 16, t & 1, lane, fb0[t]);
+      }
+      if (q == 1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) hfrag_issue<BL>(slot(ub + 2), wc * 32 + (t >> 1) * 16, t & 1, lane, fb1[t]);
+      }
+      if (q == 0 || q == 2) {
+        const char* sa = slot(q == 0 ? ub : ub + 3);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) hfrag_issue<AL>(sa, wr * 64 + (t >> 1) * 16, t & 1, lane, fa[t]);
+      }
+      // the next phase's reads: q0 -> B1(j), q1 -> A1(j), q2 -> none, q3 -> A0/B0(j+1)
+      if (q != 2) {
+        const int need = q == 0 ? ub + 2 : q == 1 ? ub + 3 : ub + 5;
+        if (need <= last_u) wait_halves(min(u_issue, last_u) - need);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      if (q == 0) { hfrag_tie<4>(fb0); hfrag_tie<8>(fa); }
+      if (q == 1) hfrag_tie<4>(fb1);
+      if (q == 2) hfrag_tie<8>(fa);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn) {
+            const HFrag& b = nh ? fb1[jn * 2 + ks] : fb0[jn * 2 + ks];
+            f32x4& c = acc[mh * 4 + i][nh * 2 + jn];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hfrag_val(b), hfrag_val(fa[i * 2 + ks]), c, 0, 0, 0);
+          }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
+#pragma unroll
+  for (int tm = 0; tm < 8; ++tm) {
+    const int64_t m = m0 + wr * 128 + tm * 16 + (lane & 15);
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int64_t n = n0 + wc * 64 + tn * 16 + (lane >> 4) * 4;
+      store4<CT>(p, acc[tm][tn], m, n);
+    }
+  }
+}
+
+template <int AL, int BL, int CT, int S>
+int launch8p(GemmArgs p, hipStream_t s) {
+  const int smem = S * kHalf;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm8p_k<AL, BL, CT, S>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_n = (int)cdiv(p.N, 256);
+  gemm8p_k<AL, BL, CT, S><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemm8p");
+}
+
 template <int AL, int BL, int CT>
 int launch(const GemmArgs& p, hipStream_t s) {
   const int smem = 4 * kTileBytes;
@@ -482,7 +754,13 @@ int launch256(GemmArgs p, hipStream_t s) {
 // so a grid of 544 tiles takes 3 rounds for 2.125 rounds of work. Per-tile rates (TFLOP/s,
 // measured on MI355X with tools/gemm_bench.py): 256x256 ~1250, 192x256
 // ~1190 (A K-contiguous only), 128x128 4-wave (2 blocks/CU, 512 slots) ~840.
-enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3 };
+// kT8p / kT8p10 (the ping-pong kernel) are selectable but not auto-chosen: measured against
+// the 2-stage kernels on the model's shapes (tools/gemm_bench.py, several boxes) they win
+// 3-7 % on big-N forward products (q|k|v, lm_head), lose 10-25 % on dX, dW and N = 4096,
+// and the box-to-box spread (~10 %) is larger than their forward gain. With the steady DMA
+// removed the same schedule reaches hipBLASLt's rate (gate|up 1483 vs 1382 TF/s), so the
+// remaining loss is LDS-DMA issue cost inside the load segment (profiles/r01/gemm_8phase.md).
+enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5 };
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
@@ -510,14 +788,14 @@ static int g_force_tile = -1;
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = (mode >= 0 && mode <= 3) ? mode : -1;
+  g_force_tile = (mode >= 0 && mode <= 5) ? mode : -1;
   return prev;
 }
 
 extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid) {
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
-  static const int bm[4] = {128, 256, 256, 192}, bn[4] = {128, 128, 256, 256};
+  static const int bm[6] = {128, 256, 256, 192, 256, 256}, bn[6] = {128, 128, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -556,6 +834,16 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
   const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
   int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  if (tile == kT8p || tile == kT8p10) {
+#define L8P(AL, BL)                                                                                          \
+  if (tile == kT8p) return f32 ? launch8p<AL, BL, CULLAVO_DT_F32, 8>(p, s) : launch8p<AL, BL, CULLAVO_DT_BF16, 8>(p, s); \
+  return f32 ? launch8p<AL, BL, CULLAVO_DT_F32, 10>(p, s) : launch8p<AL, BL, CULLAVO_DT_BF16, 10>(p, s);
+    if (a_layout == 0 && b_layout == 0) { L8P(0, 0) }
+    if (a_layout == 0 && b_layout == 1) { L8P(0, 1) }
+    if (a_layout == 1 && b_layout == 0) { L8P(1, 0) }
+    L8P(1, 1)
+#undef L8P
+  }
   if (tile != kT128) {
 #define L256(AL, BL)                                                                                         \
   if (tile == kT256x256) return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256>(p, s); \

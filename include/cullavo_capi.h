@@ -66,8 +66,9 @@ int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
 
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
  * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
- * staged; 3 falls back to 2 when A is not K-contiguous). Returns the previous
- * mode. For tests and tuning; not thread-safe. */
+ * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel
+ * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers).
+ * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls. */

@@ -43,7 +43,7 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, -1], ids=["t128", "t256x128", "t256x256", "t192x256", "auto"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, -1], ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "auto"])
 def tile_mode(request):
     from cullavo_amd import _lib
     prev = _lib.lib().cullavo_gemm_set_tile(request.param)
@@ -106,6 +106,31 @@ def test_gemm_strided_operands(tile_mode):
     xv = big.to(DEV)[:, K:2 * K]
     y = ops().linear(xv, w.to(DEV))
     close(y, big[:, K:2 * K].float() @ w.float().T, 8e-3, "strided")
+
+
+@pytest.mark.parametrize("al,bl", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_pipelined_repeatable(al, bl):
+    """Race screen for the counted-vmcnt kernels: the same product, launched many times
+    back to back at sizes with K tails and several K-tiles, must be bit-identical every time
+    (a read racing its LDS-DMA shows up as rare wrong tiles) and match the fp32 product."""
+    from cullavo_amd import _lib
+    for mode in (2, 4, 5):
+        prev = _lib.lib().cullavo_gemm_set_tile(mode)
+        try:
+            for (M, N, K) in [(768, 1024, 4160), (520, 264, 200), (2048, 2048, 1024)]:
+                A, B = rnd((M, K), 21), rnd((N, K), 22)
+                Ad = (A if al == 0 else A.T.contiguous()).to(DEV)
+                Bd = (B if bl == 0 else B.T.contiguous()).to(DEV)
+                outs = []
+                for _ in range(12):
+                    C = torch.empty((M, N), dtype=BF, device=DEV)
+                    ops().gemm(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), C, N)
+                    outs.append(C)
+                close(outs[0], A.float() @ B.float().T, 8e-3, f"mode {mode} {al}{bl} {M}x{N}x{K}")
+                for o in outs[1:]:
+                    assert torch.equal(o, outs[0]), (mode, al, bl, M, N, K)
+        finally:
+            _lib.lib().cullavo_gemm_set_tile(prev)
 
 
 # ---------------------------------------------------------------------------------------------
