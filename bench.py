@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8, help="samples per GPU")
     ap.add_argument("--config", default="llava-1.5-7b")
-    ap.add_argument("--trainable", default="full", choices=["full", "reference"])
+    ap.add_argument("--trainable", default="full", choices=["full", "reference", "lora"])
     ap.add_argument("--text-len", type=int, default=513)
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -225,7 +225,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (seeded ids/pixels/labels in HBM, random-init weights)",
             "config": {"workload": f"config 3: ViT-L/14-336 + Vicuna-7B, seq 576+512 (L={args.text_len + 575}), "
-                                   f"bs={args.batch}/GPU, bf16, {args.trainable} fine-tune (vision frozen), AdamW",
+                                   f"bs={args.batch}/GPU, bf16, {args.trainable} fine-tune "
+                                   f"({'LoRA r=64 on the LM + ViT layers 12-22' if args.trainable == 'lora' else 'vision frozen'}), AdamW",
                        "model": args.config, "global_batch": world * args.batch,
                        "seq_len": args.text_len + cfg.vision_config.num_patches - 1,
                        "parallelism": f"dp{world}", "trainable": args.trainable},

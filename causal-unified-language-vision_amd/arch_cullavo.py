@@ -17,6 +17,7 @@ from torch import nn
 from . import ops
 from .config import CuLLaVOConfig
 from .functions import HeadLossFn, MergeFn, StepContext
+from .lora import LoraSettings
 from .modeling import (CLIPVisionModel, LlamaForCausalLM, LlavaMultiModalProjector, build_arenas, init_random_)
 
 
@@ -41,18 +42,24 @@ class CullavoCausalLMOutputWithPast:
 
 class CuLLaVOModel(nn.Module):
     def __init__(self, config: CuLLaVOConfig, *, device="cuda", trainable: str = "full", init: str = "random",
-                 seed: int = 0):
+                 seed: int = 0, lora: LoraSettings | None = None):
+        """trainable: "full" | "reference" | "lora" | "none" (modeling.TRAINABLE_POLICIES); "lora"
+        adds the reference's peft adapters (lora.LoraSettings, default r=64, alpha=16, p=0.05)."""
         super().__init__()
         if config.vision_config.hidden_act != "quick_gelu" or config.projector_hidden_act != "gelu":
             raise ValueError("CuLLaVO path: CLIP quick_gelu + projector gelu")
         self.config = config
-        self.arenas = build_arenas(config, device, trainable)
+        if trainable == "lora" and lora is None:
+            lora = LoraSettings()
+        self.lora_settings = lora if trainable == "lora" else None
+        self.arenas = build_arenas(config, device, trainable, lora=self.lora_settings)
         if init == "random":
             init_random_(self.arenas, seed)
-        self.vision_tower = CLIPVisionModel(config.vision_config, self.arenas["vision"])
+        la = (self.arenas["lora"], self.lora_settings) if "lora" in self.arenas else None
+        self.vision_tower = CLIPVisionModel(config.vision_config, self.arenas["vision"], la)
         self.multi_modal_projector = LlavaMultiModalProjector(self.arenas["projector"].params)
         self.language_model = LlamaForCausalLM(config.text_config, self.arenas["embed"], self.arenas["layers"],
-                                               self.arenas["head"])
+                                               self.arenas["head"], la)
         self.trainable_policy = trainable
 
     # -- reference API -------------------------------------------------------------------------
@@ -70,10 +77,12 @@ class CuLLaVOModel(nn.Module):
             ar.zero_grad()
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
-        """Load llava-hf (transformers ~4.37) keys; copies into the arenas in place."""
+        """Load llava-hf (transformers ~4.37) keys; copies into the arenas in place. peft-wrapped
+        keys (`<linear>.base_layer.weight`) map to the base weight."""
         own = {}
         for ar in self.arenas.values():
             own.update(ar.params)
+        state_dict = {k.replace(".base_layer.", "."): v for k, v in state_dict.items()}
         missing = [k for k in own if k not in state_dict]
         unexpected = [k for k in state_dict if k not in own]
         if strict and (missing or unexpected):

@@ -24,6 +24,27 @@ DEV float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
 DEV u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 DEV float round_bf(float f) { return bf2f(f2bf(f)); }
 
+// ---- LoRA dropout mask ------------------------------------------------------------------------
+// Counter-based, so the forward (operand staging), dA (operand staging) and dX (GEMM epilogue)
+// regenerate the same mask from (seed, token, feature) without storing it. Element kept iff
+// (hash >> 8) >= thr24 = round(p * 2^24); kept values are scaled by 1/(1-p) (nn.Dropout).
+// tests/test_lora.py restates the hash in numpy and checks the masks bit-exactly.
+DEV uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+DEV uint32_t drop_hash(uint64_t seed, uint32_t token, uint32_t feat) {
+  const uint32_t h = fmix32((uint32_t)seed ^ fmix32(token * 0x9E3779B1u + (uint32_t)(seed >> 32)));
+  return fmix32(h ^ (feat * 0x27D4EB2Fu + 0x165667B1u));
+}
+DEV bool drop_keep(uint64_t seed, uint32_t thr24, int64_t token, int64_t feat) {
+  return (drop_hash(seed, (uint32_t)token, (uint32_t)feat) >> 8) >= thr24;
+}
+
 template <typename T> struct Elt;
 template <> struct Elt<u16> {
   static DEV float ld(const u16* p, int64_t i) { return bf2f(p[i]); }

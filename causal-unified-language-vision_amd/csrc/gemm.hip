@@ -34,6 +34,14 @@ struct GemmArgs {
   float alpha, beta;
   int act;
   int tiles_m, tiles_n;
+  const u16* addend;  // LoRA term added after bias: v = round(round(alpha*AB + bias) + addend)
+  int64_t ld_add;
+  int drop_mode;      // 0 none, 1 A operand, 2 B operand (register-staged kernel), 3 output
+  uint32_t drop_thr;
+  float drop_scale;
+  uint64_t drop_seed;
+  float* part;        // split-K: f32 partials [gridDim.y][M][N] (register-staged kernel only)
+  int kt_per;         // K-tiles per split
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -77,6 +85,26 @@ DEV void store_tile(char* lds, const u16x8 (&r)[4]) {
       off = img1_off(k, ch >> 1) + ((ch & 1) << 4);
     }
     *reinterpret_cast<u16x8*>(lds + off) = r[i];
+  }
+}
+
+// LoRA dropout on a staged operand tile (the operand is the activation x[token][feature]):
+// layout 0 element (row gi, col gk) is (token gi, feature gk); layout 1 (k-row gk, col gi) is
+// (token gk, feature gi).
+template <int LAYOUT>
+DEV void drop_tile(const GemmArgs& p, int64_t idx0, int64_t k0, u16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = t + 256 * i;
+    int64_t tok, f0;
+    if (LAYOUT == 0) { tok = idx0 + (q >> 3); f0 = k0 + (q & 7) * 8; }
+    else { tok = k0 + (q >> 4); f0 = idx0 + (q & 15) * 8; }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = bf2f(r[i][j]);
+      r[i][j] = drop_keep(p.drop_seed, p.drop_thr, tok, f0 + j) ? f2bf(v * p.drop_scale) : (u16)0;
+    }
   }
 }
 
@@ -125,10 +153,19 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = acc[j] * p.alpha;
+  if (p.drop_mode == 3) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = drop_keep(p.drop_seed, p.drop_thr, m, n + j) ? v[j] * p.drop_scale : 0.f;
+  }
   if (p.bias) {
     const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] += bf2f(bv[j]);
+  }
+  if (p.addend) {
+    const u16x4 av = *reinterpret_cast<const u16x4*>(p.addend + m * p.ld_add + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(av[j]);
   }
   if (p.act != CULLAVO_ACT_NONE || p.preact) {
 #pragma unroll
@@ -173,7 +210,7 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
   }
 }
 
-template <int AL, int BL, int CT>
+template <int AL, int BL, int CT, int DROP = 0>
 __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #define sA(i) (smem + 2 * (i) * kTileBytes)
@@ -200,10 +237,16 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)cdiv(p.K, BK);
+  // split-K (blockIdx.y): this block's K-tile range; one split covers all of K
+  const int nk_all = (int)cdiv(p.K, BK);
+  const int kt0 = p.part ? (int)blockIdx.y * p.kt_per : 0;
+  const int nk = p.part ? min(nk_all - kt0, p.kt_per) : nk_all;
+  const int64_t kb = (int64_t)kt0 * BK;
   u16x8 ra[4], rb[4];
-  load_tile<AL>(p.A, p.lda, m0, p.M, 0, p.K, ra);
-  load_tile<BL>(p.B, p.ldb, n0, p.N, 0, p.K, rb);
+  load_tile<AL>(p.A, p.lda, m0, p.M, kb, p.K, ra);
+  load_tile<BL>(p.B, p.ldb, n0, p.N, kb, p.K, rb);
+  if (DROP == 1) drop_tile<AL>(p, m0, kb, ra);
+  if (DROP == 2) drop_tile<BL>(p, n0, kb, rb);
   store_tile<AL>(sA(0), ra);
   store_tile<BL>(sB(0), rb);
   __syncthreads();
@@ -211,9 +254,10 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
+    const int64_t k1 = kb + (int64_t)(kt + 1) * BK;
     if (more) {
-      load_tile<AL>(p.A, p.lda, m0, p.M, (int64_t)(kt + 1) * BK, p.K, ra);
-      load_tile<BL>(p.B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BK, p.K, rb);
+      load_tile<AL>(p.A, p.lda, m0, p.M, k1, p.K, ra);
+      load_tile<BL>(p.B, p.ldb, n0, p.N, k1, p.K, rb);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -229,21 +273,40 @@ __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa[tm], acc[tm][tn], 0, 0, 0);
     }
     if (more) {
+      if (DROP == 1) drop_tile<AL>(p, m0, k1, ra);
+      if (DROP == 2) drop_tile<BL>(p, n0, k1, rb);
       store_tile<AL>(sA(cur ^ 1), ra);
       store_tile<BL>(sB(cur ^ 1), rb);
     }
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds C[m][n .. n+3] --------------------------------------------------
+  // ---- epilogue: lane holds C[m][n .. n+3] (split-K: raw f32 partials, reduced later) --------
 #pragma unroll
   for (int tm = 0; tm < 4; ++tm) {
     const int64_t m = m0 + wm * 64 + tm * 16 + (lane & 15);
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) {
       const int64_t n = n0 + wn * 64 + tn * 16 + (lane >> 4) * 4;
-      store4<CT>(p, acc[tm][tn], m, n);
+      if (p.part) {
+        if (m < p.M && n < p.N)
+          *reinterpret_cast<f32x4*>(p.part + ((int64_t)blockIdx.y * p.M + m) * p.N + n) = acc[tm][tn];
+      } else {
+        store4<CT>(p, acc[tm][tn], m, n);
+      }
     }
+  }
+}
+
+// split-K reduction: fixed split order (deterministic), then the full epilogue of store4
+template <int CT>
+__global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs p, int splits) {
+  const int64_t nq = p.N / 4, total = p.M * nq;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / nq, n = (i % nq) * 4;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < splits; ++s) acc += *reinterpret_cast<const f32x4*>(p.part + ((int64_t)s * p.M + m) * p.N + n);
+    store4<CT>(p, acc, m, n);
   }
 }
 
@@ -722,15 +785,38 @@ int launch8p(GemmArgs p, hipStream_t s) {
   return cullavo_check_launch("gemm8p");
 }
 
-template <int AL, int BL, int CT>
+// Split-K plan for the register-staged kernel: products whose 128x128 tile grid cannot fill
+// the 256 CUs but whose K is long (the LoRA adapter GEMMs: N or M = r = 64, K = tokens or
+// features) are cut into K chunks of >= 4 K-tiles, enough of them for ~512 workgroups.
+int splitk_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
+  const int64_t tiles = cdiv(M, BM) * cdiv(N, BN), nk = cdiv(K, BK);
+  if (tiles >= 192 || nk < 8) return 1;
+  int64_t s = std::min<int64_t>(std::max<int64_t>(512 / tiles, 2), std::min<int64_t>(nk / 4, 32));
+  if (s < 2) return 1;
+  const int64_t per = cdiv(nk, s);
+  s = cdiv(nk, per);
+  if (kt_per) *kt_per = (int)per;
+  return (int)s;
+}
+
+template <int AL, int BL, int CT, int DROP = 0>
 int launch(const GemmArgs& p, hipStream_t s) {
   const int smem = 4 * kTileBytes;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_k<AL, BL, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)gemm_k<AL, BL, CT, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
     attr_set = true;
   }
-  gemm_k<AL, BL, CT><<<p.tiles_m * p.tiles_n, 256, smem, s>>>(p);
+  if (p.part) {
+    const int splits = (int)cdiv(cdiv(p.K, BK), p.kt_per);
+    gemm_k<AL, BL, CT, DROP><<<dim3(p.tiles_m * p.tiles_n, splits), 256, smem, s>>>(p);
+    const int64_t work = p.M * (p.N / 4);
+    const int g = (int)std::min<int64_t>(cdiv(work, 256), 4096);
+    splitk_reduce_k<CT><<<g, 256, 0, s>>>(p, splits);
+    return cullavo_check_launch("gemm splitk");
+  }
+  gemm_k<AL, BL, CT, DROP><<<p.tiles_m * p.tiles_n, 256, smem, s>>>(p);
   return cullavo_check_launch("gemm");
 }
 
@@ -801,10 +887,10 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   return tile;
 }
 
-extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K, const void* A,
-                            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
-                            float alpha, const void* bias, int act, void* preact, const void* residual,
-                            int64_t ldr, float beta, void* stream) {
+static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
+  const int a_layout = d.a_layout, b_layout = d.b_layout, c_dtype = d.c_dtype, act = d.act;
+  const int64_t M = d.M, N = d.N, K = d.K, lda = d.lda, ldb = d.ldb, ldc = d.ldc, ldr = d.ldr;
+  const void* residual = d.residual;
   CV_REQUIRE(a_layout == 0 || a_layout == 1, CULLAVO_EINVAL, "a_layout");
   CV_REQUIRE(b_layout == 0 || b_layout == 1, CULLAVO_EINVAL, "b_layout");
   CV_REQUIRE(M >= 0 && N >= 0 && K >= 0, CULLAVO_EINVAL, "negative size");
@@ -818,15 +904,38 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
              CULLAVO_EINVAL, "leading dimension too small");
   CV_REQUIRE(c_dtype == CULLAVO_DT_BF16 || c_dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "c_dtype");
   CV_REQUIRE(act >= CULLAVO_ACT_NONE && act <= CULLAVO_ACT_QUICK_GELU, CULLAVO_EINVAL, "act");
+  CV_REQUIRE(d.addend == nullptr || (d.ld_addend % 4 == 0 && d.ld_addend >= N), CULLAVO_EINVAL,
+             "ld_addend must be >= N and a multiple of 4");
+  CV_REQUIRE(d.drop_operand >= 0 && d.drop_operand <= 3, CULLAVO_EINVAL, "drop_operand");
+  CV_REQUIRE(d.drop_operand == 0 || (d.drop_p >= 0.f && d.drop_p < 1.f), CULLAVO_EINVAL, "drop_p must be in [0, 1)");
+  CV_REQUIRE(d.drop_operand != 1 || a_layout == 0, CULLAVO_EUNSUPPORTED, "dropout on A needs a_layout 0");
+  CV_REQUIRE(d.drop_operand != 2 || b_layout == 1, CULLAVO_EUNSUPPORTED, "dropout on B needs b_layout 1");
   if (M == 0 || N == 0) return CULLAVO_OK;
   const int64_t tm = cdiv(M, BM), tn = cdiv(N, BN);
   CV_REQUIRE(tm * tn < (1ll << 31), CULLAVO_EINVAL, "too many tiles");
   GemmArgs p;
-  p.A = (const u16*)A; p.B = (const u16*)B; p.C = C;
-  p.bias = (const u16*)bias; p.preact = (u16*)preact; p.residual = (const u16*)residual;
+  p.A = (const u16*)d.A; p.B = (const u16*)d.B; p.C = d.C;
+  p.bias = (const u16*)d.bias; p.preact = (u16*)d.preact; p.residual = (const u16*)residual;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldr = ldr;
-  p.alpha = alpha; p.beta = beta; p.act = act;
+  p.alpha = d.alpha; p.beta = d.beta; p.act = act;
   p.tiles_m = (int)tm; p.tiles_n = (int)tn;
+  p.addend = (const u16*)d.addend; p.ld_add = d.ld_addend;
+  const bool dropping = d.drop_operand != 0 && d.drop_p > 0.f;
+  p.drop_mode = dropping ? d.drop_operand : 0;
+  p.drop_thr = (uint32_t)(d.drop_p * 16777216.0f + 0.5f);
+  p.drop_scale = dropping ? 1.f / (1.f - d.drop_p) : 1.f;
+  p.drop_seed = d.drop_seed;
+  p.part = nullptr;
+  p.kt_per = 0;
+  {
+    int per = 0;
+    const int splits = splitk_plan(M, N, K, &per);
+    const int64_t need = (int64_t)splits * M * N * 4;
+    if (splits > 1 && d.workspace != nullptr && d.workspace_bytes >= need && g_force_tile < 0) {
+      p.part = (float*)d.workspace;
+      p.kt_per = per;
+    }
+  }
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
@@ -834,6 +943,12 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
   const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
   int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  if (p.part) tile = kT128;
+  if (p.drop_mode == 1) return f32 ? launch<0, 0, CULLAVO_DT_F32, 1>(p, s) : launch<0, 0, CULLAVO_DT_BF16, 1>(p, s);
+  if (p.drop_mode == 2) {
+    if (a_layout == 0) return f32 ? launch<0, 1, CULLAVO_DT_F32, 2>(p, s) : launch<0, 1, CULLAVO_DT_BF16, 2>(p, s);
+    return f32 ? launch<1, 1, CULLAVO_DT_F32, 2>(p, s) : launch<1, 1, CULLAVO_DT_BF16, 2>(p, s);
+  }
   if (tile == kT8p || tile == kT8p10) {
 #define L8P(AL, BL)                                                                                          \
   if (tile == kT8p) return f32 ? launch8p<AL, BL, CULLAVO_DT_F32, 8>(p, s) : launch8p<AL, BL, CULLAVO_DT_BF16, 8>(p, s); \
@@ -859,4 +974,29 @@ extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, in
   if (a_layout == 0 && b_layout == 1) return f32 ? launch<0, 1, CULLAVO_DT_F32>(p, s) : launch<0, 1, CULLAVO_DT_BF16>(p, s);
   if (a_layout == 1 && b_layout == 0) return f32 ? launch<1, 0, CULLAVO_DT_F32>(p, s) : launch<1, 0, CULLAVO_DT_BF16>(p, s);
   return f32 ? launch<1, 1, CULLAVO_DT_F32>(p, s) : launch<1, 1, CULLAVO_DT_BF16>(p, s);
+}
+
+extern "C" int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K, const void* A,
+                            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
+                            float alpha, const void* bias, int act, void* preact, const void* residual,
+                            int64_t ldr, float beta, void* stream) {
+  cullavo_gemm_desc d{};
+  d.a_layout = a_layout; d.b_layout = b_layout; d.M = M; d.N = N; d.K = K;
+  d.A = A; d.lda = lda; d.B = B; d.ldb = ldb; d.C = C; d.ldc = ldc; d.c_dtype = c_dtype;
+  d.alpha = alpha; d.bias = bias; d.act = act; d.preact = preact; d.residual = residual; d.ldr = ldr;
+  d.beta = beta;
+  return gemm_impl(d, stream);
+}
+
+extern "C" size_t cullavo_gemm_desc_size(void) { return sizeof(cullavo_gemm_desc); }
+
+extern "C" size_t cullavo_gemm_workspace(const cullavo_gemm_desc* d) {
+  if (d == nullptr || d->M <= 0 || d->N <= 0 || d->K <= 0 || g_force_tile >= 0) return 0;
+  const int splits = splitk_plan(d->M, d->N, d->K, nullptr);
+  return splits > 1 ? (size_t)splits * (size_t)d->M * (size_t)d->N * 4 : 0;
+}
+
+extern "C" int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream) {
+  CV_REQUIRE(desc != nullptr, CULLAVO_EINVAL, "desc");
+  return gemm_impl(*desc, stream);
 }

@@ -70,12 +70,15 @@ class LinearFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------------------------------
 class StepContext:
-    """Per-forward shape/index state shared by the decoder layers (built once per step)."""
+    """Per-forward shape/index state shared by the decoder layers (built once per step).
+    lora_seed: this forward's LoRA-dropout seed (drawn from torch's CPU generator, so
+    torch.manual_seed makes runs repeatable; backward reuses it to regenerate the masks)."""
 
-    def __init__(self, B: int, L: int, position_ids, kv_start=None):
+    def __init__(self, B: int, L: int, position_ids, kv_start=None, lora_seed: int | None = None):
         self.B, self.L = B, L
         self.position_ids = position_ids.reshape(-1).contiguous()
         self.kv_start = kv_start
+        self.lora_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if lora_seed is None else lora_seed
 
 
 class LlamaLayerFn(torch.autograd.Function):
@@ -86,37 +89,46 @@ class LlamaLayerFn(torch.autograd.Function):
         H, D = cfg.num_attention_heads, cfg.head_dim
         Fd = cfg.intermediate_size
         grad = _needs_grad(ctx)
+        lg, tr, seed = layer.lora_groups, layer.training, sctx.lora_seed
         x1, rstd1 = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
-        qkv = ops.linear(x1, layer.w_qkv())  # [T, 3d]: q | k | v
+        t, u_qkv = lg["qkv"].forward(x1, tr, seed)
+        qkv = ops.linear(x1, layer.w_qkv(), addend=t)  # [T, 3d]: q | k | v
         q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
         ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
         o, lse = ops.attn_fwd(q, k, v, B=sctx.B, H=H, Lq=sctx.L, Lk=sctx.L, D=D, scale=D ** -0.5, causal=True,
                               kv_start=sctx.kv_start)
-        h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h)
+        t, u_o = lg["o"].forward(o, tr, seed)
+        h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h, addend=t)
         x2, rstd2 = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
-        gu = ops.linear(x2, layer.w_gu())  # [T, 2F]: gate | up
+        t, u_gu = lg["gu"].forward(x2, tr, seed)
+        gu = ops.linear(x2, layer.w_gu(), addend=t)  # [T, 2F]: gate | up
         a = ops.swiglu_fwd(gu)
-        h3 = ops.linear(a, layer.mlp.down_proj.weight, residual=h2)
+        t, u_d = lg["down"].forward(a, tr, seed)
+        h3 = ops.linear(a, layer.mlp.down_proj.weight, residual=h2, addend=t)
+        del t
         if grad:
-            ctx.layer, ctx.sctx = layer, sctx
-            ctx.saved = (h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a)
+            ctx.layer, ctx.sctx, ctx.train = layer, sctx, tr
+            ctx.saved = (h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a, u_qkv, u_o, u_gu, u_d)
         return h3
 
     @staticmethod
     def backward(ctx, dh3):
         layer, sctx = ctx.layer, ctx.sctx
         cfg = layer.cfg
-        h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a = ctx.saved
+        h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a, u_qkv, u_o, u_gu, u_d = ctx.saved
         ctx.saved = None
+        lg, tr, seed = layer.lora_groups, ctx.train, sctx.lora_seed
         T, d = h.shape
         H, D = cfg.num_attention_heads, cfg.head_dim
         dh3 = dh3.contiguous()
         # MLP
         da = ops.linear_dx(dh3, layer.mlp.down_proj.weight)
+        lg["down"].backward(dh3, a, u_d, da, tr, seed)
         _write_dw(dh3, a, layer.mlp.down_proj.weight)
         dgu = ops.swiglu_bwd(da, gu)
         del da
         dx2 = ops.linear_dx(dgu, layer.w_gu())
+        lg["gu"].backward(dgu, x2, u_gu, dx2, tr, seed)
         if trainable(layer.mlp.gate_proj.weight):
             g, beta = layer.gu_grad_slot()
             ops.linear_dw(dgu, x2, g, beta=beta)
@@ -129,6 +141,7 @@ class LlamaLayerFn(torch.autograd.Function):
         del dx2
         # attention
         do = ops.linear_dx(dh2, layer.self_attn.o_proj.weight)
+        lg["o"].backward(dh2, o, u_o, do, tr, seed)
         _write_dw(dh2, o, layer.self_attn.o_proj.weight)
         dqkv = torch.empty_like(qkv)
         q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
@@ -138,6 +151,7 @@ class LlamaLayerFn(torch.autograd.Function):
         ops.rope(dqkv[:, :d], dqkv[:, d:2 * d], sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta,
                  inverse=True)
         dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+        lg["qkv"].backward(dqkv, x1, u_qkv, dx1, tr, seed)
         if trainable(layer.self_attn.q_proj.weight):
             g, beta = layer.qkv_grad_slot()
             ops.linear_dw(dqkv, x1, g, beta=beta)
@@ -154,23 +168,31 @@ class LlamaLayerFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------------------------
 class ClipLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, layer, B: int, T: int, *params):
+    def forward(ctx, h, layer, B: int, T: int, lora_seed: int, *params):
         cfg = layer.cfg
         d = cfg.hidden_size
         H, D = cfg.num_attention_heads, cfg.head_dim
         grad = _needs_grad(ctx)
+        lg, tr = layer.lora_groups, layer.training
         sa, mlp = layer.self_attn, layer.mlp
         x1, m1, r1 = ops.layernorm_fwd(h, layer.layer_norm1.weight, layer.layer_norm1.bias, cfg.layer_norm_eps)
-        qkv = ops.linear(x1, layer.w_qkv(), layer.b_qkv())
+        t, u_qkv = lg["qkv"].forward(x1, tr, lora_seed)
+        qkv = ops.linear(x1, layer.w_qkv(), layer.b_qkv(), addend=t)
         q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
         o, lse = ops.attn_fwd(q, k, v, B=B, H=H, Lq=T, Lk=T, D=D, scale=D ** -0.5, causal=False)
         h2 = ops.linear(o, sa.out_proj.weight, sa.out_proj.bias, residual=h)
         x2, m2, r2 = ops.layernorm_fwd(h2, layer.layer_norm2.weight, layer.layer_norm2.bias, cfg.layer_norm_eps)
-        a, pre = _lin_act(x2, mlp.fc1.weight, mlp.fc1.bias, ACT_QUICK_GELU, grad)
-        h3 = ops.linear(a, mlp.fc2.weight, mlp.fc2.bias, residual=h2)
+        t, u_1 = lg["fc1"].forward(x2, tr, lora_seed)
         if grad:
-            ctx.layer, ctx.B, ctx.T = layer, B, T
-            ctx.saved = (h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre)
+            a, pre = ops.linear(x2, mlp.fc1.weight, mlp.fc1.bias, act=ACT_QUICK_GELU, want_preact=True, addend=t)
+        else:
+            a, pre = ops.linear(x2, mlp.fc1.weight, mlp.fc1.bias, act=ACT_QUICK_GELU, addend=t), None
+        t, u_2 = lg["fc2"].forward(a, tr, lora_seed)
+        h3 = ops.linear(a, mlp.fc2.weight, mlp.fc2.bias, residual=h2, addend=t)
+        del t
+        if grad:
+            ctx.layer, ctx.B, ctx.T, ctx.train, ctx.seed = layer, B, T, tr, lora_seed
+            ctx.saved = (h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre, u_qkv, u_1, u_2)
         return h3
 
     @staticmethod
@@ -179,15 +201,18 @@ class ClipLayerFn(torch.autograd.Function):
         cfg = layer.cfg
         d = cfg.hidden_size
         H, D = cfg.num_attention_heads, cfg.head_dim
-        h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre = ctx.saved
+        h, x1, m1, r1, qkv, o, lse, h2, x2, m2, r2, a, pre, u_qkv, u_1, u_2 = ctx.saved
         ctx.saved = None
+        lg, tr, seed = layer.lora_groups, ctx.train, ctx.seed
         sa, mlp = layer.self_attn, layer.mlp
         dh3 = dh3.contiguous()
         da = ops.linear_dx(dh3, mlp.fc2.weight)
+        lg["fc2"].backward(dh3, a, u_2, da, tr, seed)
         _write_dw(dh3, a, mlp.fc2.weight)
         _write_bias(dh3, mlp.fc2.bias)
         dpre = ops.act_bwd(ACT_QUICK_GELU, da, pre)
         dx2 = ops.linear_dx(dpre, mlp.fc1.weight)
+        lg["fc1"].backward(dpre, x2, u_1, dx2, tr, seed)
         _write_dw(dpre, x2, mlp.fc1.weight)
         _write_bias(dpre, mlp.fc1.bias)
         ln2 = layer.layer_norm2
@@ -200,7 +225,8 @@ class ClipLayerFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, B=B, H=H, Lq=T, Lk=T, D=D,
                      scale=D ** -0.5, causal=False, dq=dqkv[:, :d], dk=dqkv[:, d:2 * d], dv=dqkv[:, 2 * d:])
-        dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+        dx1 = ops.linear_dx(dqkv, layer.w_qkv()) if ctx.needs_input_grad[0] else None
+        lg["qkv"].backward(dqkv, x1, u_qkv, dx1, tr, seed)
         if trainable(sa.q_proj.weight):
             g, beta = layer.qkv_grad_slot()
             ops.linear_dw(dqkv, x1, g, beta=beta)
@@ -209,10 +235,14 @@ class ClipLayerFn(torch.autograd.Function):
             commit(sa.q_proj.weight, sa.k_proj.weight, sa.v_proj.weight, sa.q_proj.bias, sa.k_proj.bias,
                    sa.v_proj.bias)
         ln1 = layer.layer_norm1
-        dw1, db1, beta1 = _ln_slots(ln1)
-        dh = ops.layernorm_bwd(dx1, h, ln1.weight, m1, r1, dres=dh2, dw=dw1, db=db1, beta=beta1)
-        commit(ln1.weight, ln1.bias)
-        return (dh, None, None, None) + (None,) * len(layer.fn_params())
+        dh = None
+        if ctx.needs_input_grad[0] or trainable(ln1.weight):
+            dw1, db1, beta1 = _ln_slots(ln1)
+            if dx1 is None:
+                dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+            dh = ops.layernorm_bwd(dx1, h, ln1.weight, m1, r1, dres=dh2, dw=dw1, db=db1, beta=beta1)
+            commit(ln1.weight, ln1.bias)
+        return (dh, None, None, None, None) + (None,) * len(layer.fn_params())
 
 
 def _ln_slots(ln):

@@ -18,6 +18,7 @@ from . import ops
 from .arena import ParamArena
 from .config import CLIPVisionConfig, CuLLaVOConfig, LlamaConfig
 from .functions import (ClipLayerFn, EmbeddingFn, LinearFn, LlamaLayerFn, ProjectorFn, StepContext)
+from .lora import NO_LORA, LoraGroup, LoraSettings, lm_groups, lora_specs, vision_groups
 
 
 class _Box(nn.Module):
@@ -38,8 +39,38 @@ class Linear(nn.Module):
     def out_features(self):
         return self.weight.shape[0]
 
+    def attach_lora(self, arena, module_prefix: str, s: LoraSettings):
+        """peft-style adapter attributes: lora_A.<adapter>.weight, lora_B.<adapter>.weight,
+        scaling[adapter] (views into the LoRA arena; the fused layer Functions run them)."""
+        self.lora_A, self.lora_B = _Box(), _Box()
+        for box, kind in ((self.lora_A, "lora_A"), (self.lora_B, "lora_B")):
+            sub = _Box()
+            sub.weight = arena.params[f"{module_prefix}{kind}.{s.adapter}.weight"]
+            setattr(box, s.adapter, sub)
+        self.scaling = {s.adapter: s.scaling}
+        self.r = {s.adapter: s.r}
+        self.lora_dropout_p = {s.adapter: s.lora_dropout}
+
     def forward(self, x):
+        if hasattr(self, "lora_A"):
+            raise NotImplementedError("LoRA-adapted Linears run inside their layer's fused Function")
         return LinearFn.apply(x, self.weight, self.bias)
+
+
+def _attach_groups(layer, groups_def, lora, prefix: str, uid0: int):
+    """Build the layer's LoraGroups (or NO_LORA stand-ins) and the peft attributes of its Linears."""
+    layer.lora_groups = {}
+    for gi, (name, mods) in enumerate(groups_def):
+        if lora is None:
+            layer.lora_groups[name] = NO_LORA
+            continue
+        arena, s = lora
+        layer.lora_groups[name] = LoraGroup(arena, prefix, mods, s, uid0 + gi)
+        for suf, _, _ in mods:
+            mod = layer
+            for part in suf.split("."):
+                mod = getattr(mod, part)
+            mod.attach_lora(arena, prefix + suf + ".", s)
 
 
 class _NormFn(torch.autograd.Function):
@@ -137,7 +168,7 @@ def llama_layer_specs(cfg: LlamaConfig, prefix: str):
 # CLIP vision tower (tf:models/clip/modeling_clip.py:202-651)
 # ---------------------------------------------------------------------------------------------
 class CLIPEncoderLayer(nn.Module):
-    def __init__(self, cfg: CLIPVisionConfig, P: dict, lp: str, arena: ParamArena):
+    def __init__(self, cfg: CLIPVisionConfig, P: dict, lp: str, arena: ParamArena, lora=None, uid0: int = 0):
         super().__init__()
         self.cfg = cfg
         self._arena, self._lp = arena, lp
@@ -153,6 +184,7 @@ class CLIPEncoderLayer(nn.Module):
         self.layer_norm2 = LayerNorm(P[lp + "layer_norm2.weight"], P[lp + "layer_norm2.bias"], cfg.layer_norm_eps)
         arena.check_adjacent([lp + f"self_attn.{n}_proj.weight" for n in "qkv"])
         arena.check_adjacent([lp + f"self_attn.{n}_proj.bias" for n in "qkv"])
+        _attach_groups(self, vision_groups(cfg), lora, lp, uid0)
 
     def w_qkv(self):
         d = self.cfg.hidden_size
@@ -177,8 +209,8 @@ class CLIPEncoderLayer(nn.Module):
     def fn_params(self):
         return [p for p in self.parameters() if p.requires_grad]
 
-    def run(self, h2d, B, T):
-        return ClipLayerFn.apply(h2d, self, B, T, *self.fn_params())
+    def run(self, h2d, B, T, lora_seed: int = 0):
+        return ClipLayerFn.apply(h2d, self, B, T, lora_seed, *self.fn_params())
 
     def forward(self, hidden_states, attention_mask=None, causal_attention_mask=None, **kw):
         if attention_mask is not None or causal_attention_mask is not None:
@@ -198,7 +230,7 @@ class CLIPVisionOutput:
 
 
 class CLIPVisionTransformer(nn.Module):
-    def __init__(self, cfg: CLIPVisionConfig, P: dict, prefix: str, arena: ParamArena):
+    def __init__(self, cfg: CLIPVisionConfig, P: dict, prefix: str, arena: ParamArena, lora=None):
         super().__init__()
         self.cfg = cfg
         emb = _Box()
@@ -211,7 +243,10 @@ class CLIPVisionTransformer(nn.Module):
         self.pre_layrnorm = LayerNorm(P[prefix + "pre_layrnorm.weight"], P[prefix + "pre_layrnorm.bias"],
                                       cfg.layer_norm_eps)
         enc = _Box()
-        enc.layers = nn.ModuleList([CLIPEncoderLayer(cfg, P, f"{prefix}encoder.layers.{i}.", arena)
+        def _lora(i):
+            return lora if lora is not None and i in lora[1].vision_layers and lora[1].vision else None
+        enc.layers = nn.ModuleList([CLIPEncoderLayer(cfg, P, f"{prefix}encoder.layers.{i}.", arena, _lora(i),
+                                                     uid0=(1 << 20) + 8 * i)
                                     for i in range(cfg.num_hidden_layers)])
         self.encoder = enc
         self.post_layernorm = LayerNorm(P[prefix + "post_layernorm.weight"], P[prefix + "post_layernorm.bias"],
@@ -256,10 +291,10 @@ class CLIPVisionTransformer(nn.Module):
 
 
 class CLIPVisionModel(nn.Module):
-    def __init__(self, cfg: CLIPVisionConfig, arena: ParamArena):
+    def __init__(self, cfg: CLIPVisionConfig, arena: ParamArena, lora=None):
         super().__init__()
         self.config = cfg
-        self.vision_model = CLIPVisionTransformer(cfg, arena.params, "vision_tower.vision_model.", arena)
+        self.vision_model = CLIPVisionTransformer(cfg, arena.params, "vision_tower.vision_model.", arena, lora)
 
     def forward(self, pixel_values, output_hidden_states=None, **kw):
         return self.vision_model(pixel_values, output_hidden_states=output_hidden_states)
@@ -290,7 +325,7 @@ class LlavaMultiModalProjector(nn.Module):
 # Llama causal LM (tf:models/llama/modeling_llama.py:53-480)
 # ---------------------------------------------------------------------------------------------
 class LlamaDecoderLayer(nn.Module):
-    def __init__(self, cfg: LlamaConfig, P: dict, lp: str, arena: ParamArena):
+    def __init__(self, cfg: LlamaConfig, P: dict, lp: str, arena: ParamArena, lora=None, uid0: int = 0):
         super().__init__()
         self.cfg = cfg
         self._arena, self._lp = arena, lp
@@ -306,6 +341,7 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(P[lp + "post_attention_layernorm.weight"], cfg.rms_norm_eps)
         arena.check_adjacent([lp + f"self_attn.{n}_proj.weight" for n in "qkv"])
         arena.check_adjacent([lp + "mlp.gate_proj.weight", lp + "mlp.up_proj.weight"])
+        _attach_groups(self, lm_groups(cfg), lora if lora is not None and lora[1].lm else None, lp, uid0)
 
     def w_qkv(self):
         d = self.cfg.hidden_size
@@ -334,12 +370,13 @@ class LlamaDecoderLayer(nn.Module):
 
 
 class LlamaModel(nn.Module):
-    def __init__(self, cfg: LlamaConfig, embed_arena: ParamArena, layer_arena: ParamArena):
+    def __init__(self, cfg: LlamaConfig, embed_arena: ParamArena, layer_arena: ParamArena, lora=None):
         super().__init__()
         self.config = cfg
         self.embed_tokens = _Embedding(embed_arena.params["language_model.model.embed_tokens.weight"])
         P = layer_arena.params
-        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, P, f"language_model.model.layers.{i}.", layer_arena)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, P, f"language_model.model.layers.{i}.", layer_arena,
+                                                       lora, uid0=8 * i)
                                      for i in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(P["language_model.model.norm.weight"], cfg.rms_norm_eps)
 
@@ -377,10 +414,10 @@ class CausalLMOutput:
 
 
 class LlamaForCausalLM(nn.Module):
-    def __init__(self, cfg: LlamaConfig, embed_arena, layer_arena, head_arena):
+    def __init__(self, cfg: LlamaConfig, embed_arena, layer_arena, head_arena, lora=None):
         super().__init__()
         self.cfg = self.config = cfg
-        self.model = LlamaModel(cfg, embed_arena, layer_arena)
+        self.model = LlamaModel(cfg, embed_arena, layer_arena, lora)
         self.lm_head = Linear(head_arena.params["language_model.lm_head.weight"])
 
     def head_params(self):
@@ -424,11 +461,15 @@ TRAINABLE_POLICIES = {
     # the reference's non-LoRA trainable set (cullavo/load_cullavo.py:128-138): projector,
     # lm_head and embed_tokens; base weights frozen (LoRA adapters: SURVEY.md §8(f) row 1)
     "reference": {"vision": False, "projector": True, "embed": True, "layers": False, "head": True},
+    # what the reference actually trains: the "reference" set plus LoRA adapters on the LM and on
+    # ViT layers 12-22 (cullavo/load_cullavo.py:94-138)
+    "lora": {"vision": False, "projector": True, "embed": True, "layers": False, "head": True, "lora": True},
     "none": {"vision": False, "projector": False, "embed": False, "layers": False, "head": False},
 }
 
 
-def build_arenas(cfg: CuLLaVOConfig, device, trainable: str = "full", dtype=torch.bfloat16):
+def build_arenas(cfg: CuLLaVOConfig, device, trainable: str = "full", dtype=torch.bfloat16,
+                 lora: LoraSettings | None = None):
     pol = TRAINABLE_POLICIES[trainable]
     v, t = cfg.vision_config, cfg.text_config
     d = t.hidden_size
@@ -447,6 +488,9 @@ def build_arenas(cfg: CuLLaVOConfig, device, trainable: str = "full", dtype=torc
         "head": ParamArena("head", [("language_model.lm_head.weight", (t.vocab_size, d))], device=device,
                            dtype=dtype, trainable=pol["head"]),
     }
+    if pol.get("lora"):
+        ar["lora"] = ParamArena("lora", lora_specs(cfg, lora or LoraSettings()), device=device, dtype=dtype,
+                                trainable=True)
     return ar
 
 
@@ -455,7 +499,11 @@ def init_random_(arenas: dict, seed: int = 0):
     0.02 biases/embeddings. Used for the synthetic-data benchmark."""
     g = torch.Generator(device=next(iter(arenas.values())).device)
     g.manual_seed(seed)
-    for ar in arenas.values():
+    for name, ar in arenas.items():
+        if name == "lora":
+            from .lora import init_lora_
+            init_lora_(ar, seed + 1)
+            continue
         for key, (o, n, shape) in ar.offsets.items():
             v = ar.flat[o:o + n]
             if key.endswith("norm.weight") or "layer_norm" in key and key.endswith("weight") or \

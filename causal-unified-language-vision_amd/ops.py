@@ -7,12 +7,14 @@ the CPU: every function requires CUDA(HIP) tensors and fails loudly otherwise.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, DT_BF16, DT_F32, call, lib
 
 __all__ = [
-    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "linear", "linear_dx", "linear_dw",
+    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "gemm_ex", "linear", "linear_dx", "linear_dw",
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "swiglu_fwd", "swiglu_bwd",
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
@@ -88,16 +90,68 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
     return C
 
 
-def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: bool = False, out=None):
-    """y = act(x @ w.T + bias) (+ residual); x [M,K] (row stride may exceed K), w [N,K]."""
+class GemmDesc(ctypes.Structure):
+    """Mirror of cullavo_gemm_desc (include/cullavo_capi.h); tests check the size against the
+    library's cullavo_gemm_desc_size()."""
+    _fields_ = [("a_layout", ctypes.c_int), ("b_layout", ctypes.c_int), ("M", ctypes.c_int64),
+                ("N", ctypes.c_int64), ("K", ctypes.c_int64), ("A", ctypes.c_void_p), ("lda", ctypes.c_int64),
+                ("B", ctypes.c_void_p), ("ldb", ctypes.c_int64), ("C", ctypes.c_void_p), ("ldc", ctypes.c_int64),
+                ("c_dtype", ctypes.c_int), ("alpha", ctypes.c_float), ("bias", ctypes.c_void_p),
+                ("act", ctypes.c_int), ("preact", ctypes.c_void_p), ("residual", ctypes.c_void_p),
+                ("ldr", ctypes.c_int64), ("beta", ctypes.c_float), ("addend", ctypes.c_void_p),
+                ("ld_addend", ctypes.c_int64), ("drop_operand", ctypes.c_int), ("drop_p", ctypes.c_float),
+                ("drop_seed", ctypes.c_uint64), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64)]
+
+
+DROP_NONE, DROP_A, DROP_B, DROP_OUT = 0, 1, 2, 3
+
+
+def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
+            alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
+            beta: float = 0.0, addend=None, ld_addend: int = 0, drop_operand: int = DROP_NONE,
+            drop_p: float = 0.0, drop_seed: int = 0, split_k: bool = True):
+    """cullavo_gemm_ex: gemm() plus the LoRA addend, dropout masks and split-K (see the header).
+    The split-K workspace comes from torch's caching allocator (kernels never allocate)."""
+    _dev(A, B, C, bias, preact, residual, addend)
+    d = GemmDesc(a_layout, b_layout, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _dt(C), float(alpha),
+                 _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _ptr(addend), ld_addend,
+                 drop_operand, float(drop_p), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, None, 0)
+    ws = None
+    if split_k:
+        nbytes = lib().cullavo_gemm_workspace(ctypes.addressof(d))
+        if nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=C.device)
+            d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
+    traced = _TRACE["key"] is not None and _TRACE["key"] == (M, N, K, a_layout, b_layout)
+    if traced:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+    call("gemm_ex", ctypes.addressof(d), _stream())
+    if traced:
+        e1.record(torch.cuda.current_stream())
+        _TRACE["events"].append((e0, e1))
+    return C
+
+
+def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: bool = False, out=None,
+           addend=None):
+    """y = act(x @ w.T + bias [+ addend]) (+ residual); x [M,K] (row stride may exceed K), w [N,K].
+    addend [M,N] is the LoRA term, added after the bias with peft's roundings."""
     M, K = x.shape
     N = w.shape[0]
     if w.shape[1] != K:
         raise ValueError(f"linear: x {tuple(x.shape)} vs w {tuple(w.shape)}")
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
     pre = torch.empty((M, N), dtype=x.dtype, device=x.device) if want_preact else None
-    gemm(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
-         residual=residual, ldr=_ld(residual) if residual is not None else 0)
+    ldr = _ld(residual) if residual is not None else 0
+    if addend is None:
+        gemm(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
+             residual=residual, ldr=ldr)
+    else:
+        if addend.shape != (M, N):
+            raise ValueError(f"linear: addend {tuple(addend.shape)} != {(M, N)}")
+        gemm_ex(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
+                residual=residual, ldr=ldr, addend=addend, ld_addend=_ld(addend))
     return (y, pre) if want_preact else y
 
 

@@ -127,7 +127,7 @@ class DefaultTrainer:
     def _initialize_accelerator(self):
         cm = self.model.cullavo_model if hasattr(self.model, "cullavo_model") else self.model
         arenas = [a for a in cm.arenas.values() if a.trainable]
-        order = ["head", "layers", "embed", "projector", "vision"]
+        order = ["head", "layers", "lora", "embed", "projector", "vision"]
         arenas.sort(key=lambda a: order.index(a.name))
         self.accel.optimizer = self.optimizer
         if self.accel.num_processes > 1:

@@ -64,6 +64,51 @@ int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
                  const void* bias, int act, void* preact,
                  const void* residual, int64_t ldr, float beta, void* stream);
 
+/* Extended GEMM for LoRA adapters (peft LoraLayer.forward on a Linear: base(x) +
+ * lora_B(lora_A(dropout(x))) * scaling; reference
+ * cullavo/load_cullavo.py:94-112). Everything cullavo_gemm takes, plus
+ *   addend [M, N] bf16 (ld_addend, multiple of 4, nullable): added after the bias with the
+ *           module chain's roundings, v = round(round(alpha*A.B^T + bias) + addend), before
+ *           preact / activation / residual;
+ *   drop_operand: 0 none; 1 dropout on A (needs a_layout 0, A[m][k] = x[token m][feature k]);
+ *           2 on B (needs b_layout 1, B[k][n] = x[token k][feature n]); 3 on the output
+ *           (token m, feature n), applied to alpha*A.B^T before bias / beta;
+ *   drop_p in [0, 1), drop_seed: element kept iff (hash(seed, token, feature) >> 8) >=
+ *           round(drop_p * 2^24), kept values scaled by 1/(1-drop_p) (csrc/common.h drop_hash).
+ * Operand dropout runs on the register-staged 128x128 kernel. Products whose tile grid cannot
+ * fill the GPU but whose K is long (the adapters' r = 64 GEMMs) run split-K when a workspace of
+ * cullavo_gemm_workspace(desc) bytes is passed: f32 partials, reduced in a fixed order. */
+typedef struct {
+  int a_layout, b_layout;
+  int64_t M, N, K;
+  const void* A;
+  int64_t lda;
+  const void* B;
+  int64_t ldb;
+  void* C;
+  int64_t ldc;
+  int c_dtype;
+  float alpha;
+  const void* bias;
+  int act;
+  void* preact;
+  const void* residual;
+  int64_t ldr;
+  float beta;
+  const void* addend;
+  int64_t ld_addend;
+  int drop_operand;
+  float drop_p;
+  uint64_t drop_seed;
+  void* workspace;          /* nullable: split-K f32 partials (size: cullavo_gemm_workspace) */
+  int64_t workspace_bytes;
+} cullavo_gemm_desc;
+int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream);
+/* sizeof(cullavo_gemm_desc) as compiled into the library (binding check) */
+size_t cullavo_gemm_desc_size(void);
+/* bytes of split-K workspace cullavo_gemm_ex would use for this problem (0: no split) */
+size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
+
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
  * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
  * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel

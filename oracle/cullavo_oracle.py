@@ -33,6 +33,7 @@ import math
 import zlib
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -262,14 +263,65 @@ def quick_gelu(x):
     return x * torch.sigmoid(1.702 * x)
 
 
-def clip_layer(h, W, prefix, cfg: VisionCfg):
-    """CLIPEncoderLayer (tf:models/clip/modeling_clip.py:353-384)"""
+# ---- LoRA (peft LoraLayer on nn.Linear; reference cullavo/load_cullavo.py:94-112) -----------------
+# peft is not vendored in the reference and is absent here: restated from its published
+# algorithm, result = base_layer(x) + lora_B(lora_A(dropout(x))) * scaling, scaling = alpha / r.
+# Parity for this row is "unpinned by the reference" (no peft run possible); the base path it
+# extends is pinned by the golden vectors.
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def lora_keep_mask(seed: int, rows: int, cols: int, p: float):
+    """numpy restatement of csrc/common.h drop_hash / drop_keep: bool [rows, cols], element
+    (token, feature) kept iff (hash >> 8) >= round(p * 2^24) (float32 arithmetic as in C)."""
+    tok = np.arange(rows, dtype=np.uint64)[:, None]
+    feat = np.arange(cols, dtype=np.uint64)[None, :]
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    t = _fmix32((tok * np.uint64(0x9E3779B1) + np.uint64(seed >> 32)) & np.uint64(_M32))
+    h = _fmix32(np.uint64(seed & _M32) ^ t)
+    h = _fmix32(h ^ ((feat * np.uint64(0x27D4EB2F) + np.uint64(0x165667B1)) & np.uint64(_M32)))
+    thr = int(np.float32(p) * np.float32(16777216.0) + np.float32(0.5))
+    return (h >> np.uint64(8)) >= np.uint64(thr)
+
+
+class LoraOracle:
+    """Adapter weights (keys `<linear>.lora_A.<adapter>.weight` in W), scaling, dropout p and
+    an optional per-module keep mask {linear path: bool [tokens, in]} (None = no dropout)."""
+
+    def __init__(self, adapter: str, scaling: float, p: float = 0.0, masks: dict | None = None):
+        self.adapter, self.scaling, self.p, self.masks = adapter, scaling, p, masks or {}
+
+
+def lora_linear(x, W, path: str, lora: LoraOracle | None, bias: bool = False):
+    """peft LoraLayer.forward around F.linear (bias='none': the adapters carry no bias)."""
+    y = F.linear(x, W[path + ".weight"], W[path + ".bias"] if bias else None)
+    if lora is None or f"{path}.lora_A.{lora.adapter}.weight" not in W:
+        return y
+    A, B = W[f"{path}.lora_A.{lora.adapter}.weight"], W[f"{path}.lora_B.{lora.adapter}.weight"]
+    xd = x
+    mask = lora.masks.get(path)
+    if mask is not None:
+        m = torch.as_tensor(mask, dtype=x.dtype).reshape(*x.shape[:-1], x.shape[-1])
+        xd = x * m / (1.0 - lora.p)
+    return y + F.linear(F.linear(xd, A), B) * lora.scaling
+
+
+def clip_layer(h, W, prefix, cfg: VisionCfg, lora: LoraOracle | None = None):
+    """CLIPEncoderLayer (tf:models/clip/modeling_clip.py:353-384), optional peft LoRA"""
     B, T, d = h.shape
     H, D = cfg.num_attention_heads, cfg.head_dim
     x = layernorm(h, W[prefix + "layer_norm1.weight"], W[prefix + "layer_norm1.bias"], cfg.layer_norm_eps)
 
     def proj(n, t):
-        return F.linear(t, W[prefix + f"self_attn.{n}.weight"], W[prefix + f"self_attn.{n}.bias"])
+        return lora_linear(t, W, prefix + f"self_attn.{n}", lora, bias=True)
 
     q = proj("q_proj", x).view(B, T, H, D).transpose(1, 2)
     k = proj("k_proj", x).view(B, T, H, D).transpose(1, 2)
@@ -277,12 +329,13 @@ def clip_layer(h, W, prefix, cfg: VisionCfg):
     o = attention(q, k, v, D ** -0.5).transpose(1, 2).reshape(B, T, d)
     h = h + proj("out_proj", o)
     x = layernorm(h, W[prefix + "layer_norm2.weight"], W[prefix + "layer_norm2.bias"], cfg.layer_norm_eps)
-    x = F.linear(x, W[prefix + "mlp.fc1.weight"], W[prefix + "mlp.fc1.bias"])
-    x = F.linear(quick_gelu(x), W[prefix + "mlp.fc2.weight"], W[prefix + "mlp.fc2.bias"])
+    x = lora_linear(x, W, prefix + "mlp.fc1", lora, bias=True)
+    x = lora_linear(quick_gelu(x), W, prefix + "mlp.fc2", lora, bias=True)
     return h + x
 
 
-def vision_hidden_states(pixel_values, W, cfg: VisionCfg, n_layers: int | None = None):
+def vision_hidden_states(pixel_values, W, cfg: VisionCfg, n_layers: int | None = None,
+                         lora: LoraOracle | None = None):
     """CLIPVisionTransformer with output_hidden_states=True; returns the tuple
     (pre_layrnorm output, layer 1 output, ..., layer n output)."""
     vp = "vision_tower.vision_model."
@@ -295,7 +348,7 @@ def vision_hidden_states(pixel_values, W, cfg: VisionCfg, n_layers: int | None =
     hs = [h]
     n = cfg.num_hidden_layers if n_layers is None else n_layers
     for i in range(n):
-        h = clip_layer(h, W, f"{vp}encoder.layers.{i}.", cfg)
+        h = clip_layer(h, W, f"{vp}encoder.layers.{i}.", cfg, lora)
         hs.append(h)
     return hs
 
@@ -346,21 +399,25 @@ def merge(image_features, inputs_embeds, input_ids, attention_mask, cfg: CuLLaVO
     return final_embedding, final_attention_mask, final_labels, position_ids
 
 
-def llama_layer(h, W, prefix, cfg: TextCfg, cos, sin, allowed):
-    """LlamaDecoderLayer (tf:models/llama/modeling_llama.py:284-345)"""
+def llama_layer(h, W, prefix, cfg: TextCfg, cos, sin, allowed, lora: LoraOracle | None = None):
+    """LlamaDecoderLayer (tf:models/llama/modeling_llama.py:284-345), optional peft LoRA"""
     B, L, d = h.shape
     H, D = cfg.num_attention_heads, cfg.head_dim
+
+    def lin(t, n):
+        return lora_linear(t, W, prefix + n, lora)
+
     x = rmsnorm(h, W[prefix + "input_layernorm.weight"], cfg.rms_norm_eps)
-    q = F.linear(x, W[prefix + "self_attn.q_proj.weight"]).view(B, L, H, D).transpose(1, 2)
-    k = F.linear(x, W[prefix + "self_attn.k_proj.weight"]).view(B, L, H, D).transpose(1, 2)
-    v = F.linear(x, W[prefix + "self_attn.v_proj.weight"]).view(B, L, H, D).transpose(1, 2)
+    q = lin(x, "self_attn.q_proj").view(B, L, H, D).transpose(1, 2)
+    k = lin(x, "self_attn.k_proj").view(B, L, H, D).transpose(1, 2)
+    v = lin(x, "self_attn.v_proj").view(B, L, H, D).transpose(1, 2)
     q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
     o = attention(q, k, v, D ** -0.5, allowed).transpose(1, 2).reshape(B, L, d)
-    h = h + F.linear(o, W[prefix + "self_attn.o_proj.weight"])
+    h = h + lin(o, "self_attn.o_proj")
     x = rmsnorm(h, W[prefix + "post_attention_layernorm.weight"], cfg.rms_norm_eps)
-    g = F.linear(x, W[prefix + "mlp.gate_proj.weight"])
-    u = F.linear(x, W[prefix + "mlp.up_proj.weight"])
-    return h + F.linear(F.silu(g) * u, W[prefix + "mlp.down_proj.weight"])
+    g = lin(x, "mlp.gate_proj")
+    u = lin(x, "mlp.up_proj")
+    return h + lin(F.silu(g) * u, "mlp.down_proj")
 
 
 def causal_allowed(attention_mask):
@@ -370,14 +427,14 @@ def causal_allowed(attention_mask):
     return (causal[None] & (attention_mask[:, None, :] != 0))[:, None]
 
 
-def llama_hidden(embeds, attention_mask, position_ids, W, cfg: TextCfg):
+def llama_hidden(embeds, attention_mask, position_ids, W, cfg: TextCfg, lora: LoraOracle | None = None):
     """LlamaModel: layers + final norm; returns (final normed hidden, per-layer hidden list)"""
     cos, sin = rope_cos_sin(position_ids, cfg.head_dim, cfg.rope_theta)
     allowed = causal_allowed(attention_mask)
     h = embeds
     hs = [h]
     for i in range(cfg.num_hidden_layers):
-        h = llama_layer(h, W, f"language_model.model.layers.{i}.", cfg, cos, sin, allowed)
+        h = llama_layer(h, W, f"language_model.model.layers.{i}.", cfg, cos, sin, allowed, lora)
         hs.append(h)
     return rmsnorm(h, W["language_model.model.norm.weight"], cfg.rms_norm_eps), hs
 
@@ -400,7 +457,8 @@ def needed_vision_layers(cfg: CuLLaVOCfg, layer: int) -> int:
 
 
 def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, labels=None,
-            vision_feature_layer=None, vision_feature_select_strategy=None):
+            vision_feature_layer=None, vision_feature_select_strategy=None, lora: LoraOracle | None = None,
+            vision_lora: LoraOracle | None = None):
     """CuLLaVOModel.forward (reference cullavo/arch_cullavo.py:546-677), training branch.
     Returns (loss or None, logits f32 [B,L,V], aux dict)."""
     layer = cfg.vision_feature_layer if vision_feature_layer is None else vision_feature_layer
@@ -409,7 +467,7 @@ def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, la
     inputs_embeds = W["language_model.model.embed_tokens.weight"][input_ids]
     # image_outputs.hidden_states[vision_feature_layer]: only layers up to that index are needed
     n_needed = needed_vision_layers(cfg, layer)
-    hs = vision_hidden_states(pixel_values, W, cfg.vision, n_needed)
+    hs = vision_hidden_states(pixel_values, W, cfg.vision, n_needed, vision_lora)
     selected = hs[n_needed]
     if strategy == "default":
         selected = selected[:, 1:]
@@ -423,7 +481,7 @@ def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, la
     embeds, mask, _, pos = merge(image_features, inputs_embeds, input_ids, attention_mask, cfg, labels)
     if labels is None:
         labels = torch.full_like(mask, cfg.ignore_index).to(torch.long)
-    hidden, lm_hs = llama_hidden(embeds, mask, pos, W, cfg.text)
+    hidden, lm_hs = llama_hidden(embeds, mask, pos, W, cfg.text, lora)
     logits = F.linear(hidden, W["language_model.lm_head.weight"]).float()
     loss = shifted_ce(logits, labels, mask)
     return loss, logits, {"attention_mask": mask, "position_ids": pos, "image_features": image_features,

@@ -1,0 +1,282 @@
+"""LoRA adapters (reference cullavo/load_cullavo.py:94-138).
+
+Parity source: peft is neither vendored in the reference nor installed here, so the oracle
+restates peft's LoraLayer (oracle/cullavo_oracle.py:lora_linear); this row is "parity unpinned
+by the reference". The base model it extends is pinned by tests/golden. Dropout masks are the
+library's counter-based hash, restated in numpy (oracle lora_keep_mask) and compared bit-exactly.
+
+Tolerances: bf16 storage (2^-8 relative step). Kernel-level outputs max|err| <= 1e-2 * scale;
+model-level loss |d| <= 3e-2, logits / gradients relative-L2 <= 3e-2 / 6e-2 (as tests/test_model_gpu.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cullavo_oracle as O
+
+BF = torch.bfloat16
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU: settings, arena layout, mask statistics
+# ---------------------------------------------------------------------------------------------
+def test_settings_match_reference():
+    from cullavo_amd.lora import LM_TARGETS, VISION_TARGETS, LoraSettings
+    s = LoraSettings()
+    assert (s.r, s.lora_alpha, s.lora_dropout) == (64, 16.0, 0.05)  # load_cullavo.py:94-110
+    assert s.scaling == 0.25
+    assert s.vision_layers == tuple(range(12, 23))  # layers_to_transform, :101
+    assert set(LM_TARGETS) == {"q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj"}
+    assert set(VISION_TARGETS) == {"q_proj", "k_proj", "v_proj", "fc1", "fc2"}  # out_proj excluded, :18-19
+
+
+def test_lora_specs_peft_keys_and_stacking():
+    from cullavo_amd.config import llava_1_5_7b
+    from cullavo_amd.lora import LoraSettings, lora_specs
+    cfg = llava_1_5_7b()
+    specs = lora_specs(cfg, LoraSettings())
+    keys = [k for k, _ in specs]
+    shp = dict(specs)
+    lp = "language_model.model.layers.0."
+    assert shp[lp + "self_attn.q_proj.lora_A.step1.weight"] == (64, 4096)
+    assert shp[lp + "mlp.down_proj.lora_A.step1.weight"] == (64, 11008)
+    assert shp[lp + "mlp.gate_proj.lora_B.step1.weight"] == (11008, 64)
+    # q|k|v lora_A adjacent (stacked [3r, in] GEMM operand), then their lora_B
+    i = keys.index(lp + "self_attn.q_proj.lora_A.step1.weight")
+    assert keys[i:i + 6] == [lp + f"self_attn.{n}_proj.lora_{ab}.step1.weight" for ab in "AB" for n in "qkv"]
+    vis = {k.split(".encoder.layers.")[1].split(".")[0] for k in keys if k.startswith("vision_tower")}
+    assert vis == {str(i) for i in range(12, 23)}
+    assert not any("out_proj" in k or "lm_head" in k for k in keys)
+    n = sum(int(np.prod(s)) for _, s in specs)
+    # LoRA-LM 159.9 M + LoRA-ViT 11.5 M trainable parameters
+    assert abs(n - (159.9e6 + 11.5e6)) / 171.4e6 < 0.01, n
+
+
+def test_keep_mask_statistics():
+    keep = O.lora_keep_mask(12345, 2048, 4096, 0.05)
+    frac = keep.mean()
+    assert abs(frac - 0.95) < 2e-3, frac
+    other = O.lora_keep_mask(12346, 2048, 4096, 0.05)
+    assert (keep != other).mean() > 0.08  # independent seeds: ~2 p (1 - p) disagree
+    # no structure along tokens or features
+    assert np.abs(keep.mean(0) - 0.95).max() < 0.05 and np.abs(keep.mean(1) - 0.95).max() < 0.03
+    assert O.lora_keep_mask(7, 16, 16, 0.0).all()
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: gemm_ex epilogue / dropout, LoraGroup, whole model
+# ---------------------------------------------------------------------------------------------
+def rnd(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(BF)
+
+
+def close(out, ref, tol, what):
+    out, ref = out.float().cpu(), ref.float().cpu()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-12
+    assert err <= tol * scale, f"{what}: max|err| {err:.3e} > {tol:.1e} * {scale:.3e}"
+
+
+@pytest.mark.gpu
+def test_desc_layout_matches_library():
+    import ctypes
+    from cullavo_amd import _lib, ops
+    assert _lib.lib().cullavo_gemm_desc_size() == ctypes.sizeof(ops.GemmDesc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", [0, 2])
+def test_gemm_addend_epilogue(act):
+    from cullavo_amd import ops
+    M, N, K = 300, 264, 192
+    x, w, b = rnd((M, K), 1), rnd((N, K), 2, 0.1), rnd((N,), 3, 0.1)
+    t, r = rnd((M, N), 4, 0.5), rnd((M, N), 5)
+    y, pre = ops.linear(x.cuda(), w.cuda(), b.cuda(), act=act, residual=r.cuda(), want_preact=True, addend=t.cuda())
+    base = (x.float() @ w.float().T + b.float()).to(BF)           # base_layer output (bf16)
+    lin = (base.float() + t.float()).to(BF).float()                # + lora term (bf16)
+    a = lin if act == 0 else O.quick_gelu(lin)
+    close(pre, lin, 8e-3, "preact")
+    close(y, a.to(BF).float() + r.float(), 8e-3, "y")
+
+
+@pytest.mark.gpu
+def test_gemm_dropout_operands_and_output():
+    from cullavo_amd import ops
+    p, seed = 0.1, 0xC0FFEE1234
+    T, F_, R = 136, 264, 64
+    keep = torch.from_numpy(O.lora_keep_mask(seed, T, F_, p)).float()
+    x = rnd((T, F_), 10)
+    xd = x.float() * keep / (1 - p)
+    A = rnd((R, F_), 11)
+    # forward operand: u = dropout(x) A^T
+    u = torch.empty((T, R), dtype=BF, device="cuda")
+    ops.gemm_ex(0, 0, T, R, F_, x.cuda(), F_, A.cuda(), F_, u, R, drop_operand=ops.DROP_A, drop_p=p, drop_seed=seed)
+    close(u, xd.to(BF).float() @ A.float().T, 1e-2, "drop A")
+    # dA = du^T dropout(x)   (A operand du layout 1, B operand x layout 1)
+    du = rnd((T, R), 12)
+    dA = torch.empty((R, F_), dtype=BF, device="cuda")
+    ops.gemm_ex(1, 1, R, F_, T, du.cuda(), R, x.cuda(), F_, dA, F_, drop_operand=ops.DROP_B, drop_p=p,
+                drop_seed=seed)
+    close(dA, du.float().T @ xd.to(BF).float(), 1e-2, "drop B")
+    # dx += mask * (du A) / (1-p)   (output mask in the epilogue, accumulating)
+    dx0 = rnd((T, F_), 13)
+    dx = dx0.cuda().clone()
+    ops.gemm_ex(0, 1, T, F_, R, du.cuda(), R, A.cuda(), F_, dx, F_, beta=1.0, drop_operand=ops.DROP_OUT, drop_p=p,
+                drop_seed=seed)
+    close(dx, dx0.float() + keep * (du.float() @ A.float()) / (1 - p), 1e-2, "drop out")
+    # the mask itself, bit-exactly: ones through the A-operand path
+    ones = torch.ones((T, F_), dtype=BF, device="cuda")
+    eye = torch.zeros((F_, F_), dtype=BF)
+    eye.fill_diagonal_(1.0)
+    got = torch.empty((T, F_), dtype=BF, device="cuda")
+    ops.gemm_ex(0, 0, T, F_, F_, ones, F_, eye.cuda(), F_, got, F_, drop_operand=ops.DROP_A, drop_p=p, drop_seed=seed)
+    assert torch.equal(got.cpu().float() != 0, keep.bool())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,al,bl", [(64, 4096, 8704, 1, 1), (8704, 64, 4096, 0, 0), (8704, 64, 11008, 0, 1),
+                                         (4096, 64, 8704, 1, 1), (200, 136, 3000, 0, 0)])
+def test_gemm_split_k(M, N, K, al, bl):
+    """The adapters' skinny products run split-K (f32 partials + fixed-order reduction): same
+    result as the fp32 product, with beta accumulation and an f32 output, bit-identical on repeat."""
+    import ctypes
+    from cullavo_amd import _lib, ops
+    d = ops.GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    assert _lib.lib().cullavo_gemm_workspace(ctypes.addressof(d)) > 0
+    A, B = rnd((M, K), 60, 0.5), rnd((N, K), 61, 0.5)
+    Ad = (A if al == 0 else A.T.contiguous()).cuda()
+    Bd = (B if bl == 0 else B.T.contiguous()).cuda()
+    C0 = rnd((M, N), 62).float()
+    C = C0.cuda().clone()
+    ops.gemm_ex(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), C, N, alpha=0.5, beta=1.0)
+    close(C, 0.5 * (A.float() @ B.float().T) + C0, 2e-3, "split-K f32 beta")
+    outs = []
+    for _ in range(3):
+        Cb = torch.empty((M, N), dtype=BF, device="cuda")
+        ops.gemm_ex(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), Cb, N)
+        outs.append(Cb)
+    close(outs[0], A.float() @ B.float().T, 8e-3, "split-K bf16")
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+
+
+def _lora_arena(n_mods, out, inn, r, seed):
+    from cullavo_amd.arena import ParamArena
+    from cullavo_amd.lora import LoraGroup, LoraSettings
+    s = LoraSettings(r=r, lora_alpha=2.0 * r, lora_dropout=0.1)
+    names = ["q_proj", "k_proj", "v_proj"][:n_mods]
+    mods = [(f"self_attn.{n}", out, inn) for n in names]
+    specs = [(f"L.self_attn.{n}.lora_A.step1.weight", (r, inn)) for n in names]
+    specs += [(f"L.self_attn.{n}.lora_B.step1.weight", (out, r)) for n in names]
+    ar = ParamArena("lora", specs, device="cuda", trainable=True)
+    with torch.no_grad():
+        for i, (k, shp) in enumerate(specs):
+            ar.params[k].copy_(rnd(shp, seed + i, 0.2))
+    return ar, LoraGroup(ar, "L.", mods, s, uid=5), s, names
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("train", [False, True])
+def test_lora_group_forward_backward(train):
+    from cullavo_amd.lora import module_seed
+    T, inn, out, r, n = 200, 256, 128, 64, 3
+    ar, grp, s, names = _lora_arena(n, out, inn, r, 40)
+    step_seed = 987654321
+    x = rnd((T, inn), 50)
+    t, u = grp.forward(x.cuda(), train, step_seed)
+    dy = rnd((T, n * out), 51)
+    dx = torch.zeros((T, inn), dtype=BF, device="cuda")
+    ar.zero_grad()
+    grp.backward(dy.cuda(), x.cuda(), u, dx, train, step_seed)
+    # fp32 autograd restatement (peft LoraLayer) on the same masks
+    xr = x.float().requires_grad_(True)
+    As = [ar.params[f"L.self_attn.{nm}.lora_A.step1.weight"].detach().float().cpu().requires_grad_(True)
+          for nm in names]
+    Bs = [ar.params[f"L.self_attn.{nm}.lora_B.step1.weight"].detach().float().cpu().requires_grad_(True)
+          for nm in names]
+    outs = []
+    for m in range(n):
+        xd = xr
+        if train:
+            keep = torch.from_numpy(O.lora_keep_mask(module_seed(step_seed, 5, m), T, inn, s.lora_dropout)).float()
+            xd = xr * keep / (1 - s.lora_dropout)
+        outs.append((xd @ As[m].T) @ Bs[m].T * s.scaling)
+    ref_t = torch.cat(outs, 1)
+    close(t, ref_t, 1.5e-2, "t")
+    ref_t.backward(dy.float())
+    close(dx, xr.grad, 1.5e-2, "dx")
+    for m, nm in enumerate(names):
+        close(ar.params[f"L.self_attn.{nm}.lora_A.step1.weight"].grad, As[m].grad, 1.5e-2, f"dA {nm}")
+        close(ar.params[f"L.self_attn.{nm}.lora_B.step1.weight"].grad, Bs[m].grad, 1.5e-2, f"dB {nm}")
+
+
+def _lora_oracle_masks(model, sctx_seed, n_tokens):
+    """The masks the model's LM adapters draw for one forward (vision tower runs in eval)."""
+    from cullavo_amd.lora import module_seed
+    masks = {}
+    s = model.lora_settings
+    for layer in model.language_model.model.layers:
+        for grp in layer.lora_groups.values():
+            for m, suf in enumerate(grp.suffixes):
+                path = grp.a_keys[m].split(".lora_A.")[0]
+                masks[path] = O.lora_keep_mask(module_seed(sctx_seed, grp.uid, m), n_tokens, grp.in_f, s.lora_dropout)
+    return masks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dropout", [0.0, 0.05])
+def test_model_lora_step_matches_oracle(dropout):
+    from cullavo_amd.arch_cullavo import CuLLaVOModel
+    from cullavo_amd.config import tiny_gpu
+    from cullavo_amd.lora import LoraSettings
+    cfg = O.config_small_gpu()
+    W = O.make_weights(cfg, 4)
+    s = LoraSettings(r=64, lora_alpha=16.0, lora_dropout=dropout, vision_layers=(1, 2))
+    m = CuLLaVOModel(tiny_gpu(), device="cuda", trainable="lora", init="random", lora=s, seed=9)
+    m.load_state_dict(W, strict=False)
+    # non-zero lora_B so every adapter term and gradient is exercised
+    with torch.no_grad():
+        g = torch.Generator(device="cuda").manual_seed(3)
+        for k, p in m.arenas["lora"].params.items():
+            if ".lora_B." in k:
+                p.normal_(0.0, 0.05, generator=g)
+    Wl = dict(W)
+    for k, p in m.arenas["lora"].params.items():
+        Wl[k] = p.detach().float().cpu().clone().requires_grad_(True)
+    for k in ("multi_modal_projector.linear_1.weight", "language_model.lm_head.weight"):
+        Wl[k] = Wl[k].clone().requires_grad_(True)
+    ids, mask, pix, labels = O.make_inputs(cfg, 2, 40, 4, 7)
+    m.train()
+    torch.manual_seed(1234)
+    out = m(input_ids=ids.cuda(), pixel_values=pix.cuda(), attention_mask=mask.cuda(), labels=labels.cuda())
+    out.loss.backward()
+    torch.manual_seed(1234)
+    step_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    B, L = out.logits.shape[:2]
+    masks = _lora_oracle_masks(m, step_seed, B * L) if dropout > 0 else {}
+    lo = O.LoraOracle("step1", s.scaling, dropout, masks)
+    lv = O.LoraOracle("step1", s.scaling, 0.0, {})  # vision tower in eval(): no dropout
+    loss_ref, logits_ref, aux = O.forward(Wl, cfg, ids, pix, mask, labels, lora=lo, vision_lora=lv)
+    loss_ref.backward()
+    assert abs(out.loss.item() - loss_ref.item()) <= 3e-2, (out.loss.item(), loss_ref.item())
+    valid = aux["attention_mask"].bool()
+    a, b = out.logits.detach().float().cpu()[valid], logits_ref.detach()[valid]
+    assert ((a - b).norm() / b.norm()).item() <= 3e-2
+    checked = 0
+    for k, p in m.arenas["lora"].params.items():
+        ref = Wl[k].grad
+        if ref is None:  # adapters above vision_feature_layer never run: no gradient
+            assert float(p.grad.float().abs().max()) == 0.0, k
+            checked += 1
+            continue
+        err = ((p.grad.float().cpu() - ref).norm() / (ref.norm() + 1e-12)).item()
+        assert err <= 6e-2, (k, err)
+        checked += 1
+    assert checked == len(m.arenas["lora"].params)
+    for k in ("multi_modal_projector.linear_1.weight", "language_model.lm_head.weight"):
+        p = m.arenas["projector" if k.startswith("multi") else "head"].params[k]
+        err = ((p.grad.float().cpu() - Wl[k].grad).norm() / Wl[k].grad.norm()).item()
+        assert err <= 6e-2, (k, err)
+    # base weights stay frozen
+    assert not m.arenas["layers"].trainable and not m.arenas["vision"].trainable
