@@ -62,6 +62,19 @@ class CuLLaVOModel(nn.Module):
                                                self.arenas["head"], la)
         self.trainable_policy = trainable
 
+    @classmethod
+    def from_pretrained(cls, path: str, *, device="cuda", trainable: str = "full", lora: LoraSettings | None = None,
+                        **kw) -> "CuLLaVOModel":
+        """llava-hf checkpoint directory (config.json + *.safetensors, ~4.37 or >= 4.45 key
+        layout) -> model, streamed into HBM (reference cullavo/load_cullavo.py:86)."""
+        from .checkpoint import load_llava_safetensors
+        m = cls(CuLLaVOConfig.from_json(path), device=device, trainable=trainable, init="none", lora=lora)
+        if "lora" in m.arenas:
+            from .lora import init_lora_
+            init_lora_(m.arenas["lora"], kw.get("seed", 0))
+        load_llava_safetensors(m, path)
+        return m
+
     # -- reference API -------------------------------------------------------------------------
     def get_input_embeddings(self):
         return self.language_model.model.embed_tokens

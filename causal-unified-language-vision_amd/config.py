@@ -62,6 +62,36 @@ class CuLLaVOConfig:
     use_return_dict: bool = True
 
     @classmethod
+    def from_json(cls, path: str) -> "CuLLaVOConfig":
+        """From a llava-hf config.json (a directory or the file) without transformers."""
+        import json
+        import os
+        from types import SimpleNamespace
+        if os.path.isdir(path):
+            path = os.path.join(path, "config.json")
+        with open(path) as f:
+            d = json.load(f)
+
+        def ns(x):
+            return SimpleNamespace(**{k: ns(v) if isinstance(v, dict) else v for k, v in x.items()})
+        hf = ns(d)
+        v = hf.vision_config
+        for k, dv in (("image_size", 336), ("patch_size", 14), ("hidden_size", 1024), ("num_hidden_layers", 24),
+                      ("num_attention_heads", 16), ("intermediate_size", 4096), ("layer_norm_eps", 1e-5),
+                      ("hidden_act", "quick_gelu")):
+            if not hasattr(v, k):
+                setattr(v, k, dv)
+        t = hf.text_config
+        for k, dv in (("hidden_size", 4096), ("num_hidden_layers", 32), ("num_attention_heads", 32),
+                      ("intermediate_size", 11008), ("vocab_size", 32064), ("rms_norm_eps", 1e-5)):
+            if not hasattr(t, k):
+                setattr(t, k, dv)
+        for k, dv in (("vision_feature_layer", -2), ("vision_feature_select_strategy", "default")):
+            if not hasattr(hf, k):
+                setattr(hf, k, dv)
+        return cls.from_hf(hf)
+
+    @classmethod
     def from_hf(cls, hf) -> "CuLLaVOConfig":
         """Build from a transformers LlavaConfig (any version with vision_config/text_config)."""
         v, t = hf.vision_config, hf.text_config

@@ -85,6 +85,20 @@ class BaseModel(nn.Module):
     def forward(self, *a, **k):
         return self.model(*a, **k)
 
+    def save_pretrained(self, save_dir, epoch, accel):
+        """reference modeling/BaseModel.py:20-69 (checkpoint.save_cullavo)"""
+        from .checkpoint import save_cullavo
+        save_cullavo(self.cullavo_model, save_dir, epoch, is_main_process=accel.is_main_process)
+        import torch.distributed as dist
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.barrier()
+
+    def from_pretrained(self, load_dir, accel=None):
+        """reference modeling/BaseModel.py:71-136 (checkpoint.load_cullavo)"""
+        from .checkpoint import load_cullavo
+        load_cullavo(self.cullavo_model, load_dir)
+        return self
+
 
 class CuLLaVOPipeline:
     def __init__(self, opt):
