@@ -123,7 +123,8 @@ class CuLLaVOModel(nn.Module):
         strategy = (vision_feature_select_strategy if vision_feature_select_strategy is not None
                     else cfg.vision_feature_select_strategy)
         if past_key_values is not None or use_cache:
-            raise NotImplementedError("KV-cache decode / generate is SURVEY.md §8(f) row 2 (not built yet)")
+            return self._forward_cached(input_ids, pixel_values, attention_mask, position_ids, past_key_values,
+                                        inputs_embeds, vision_feature_layer, strategy, labels, return_dict)
         if output_attentions:
             raise NotImplementedError("flash attention never materialises attention probabilities")
 
@@ -160,6 +161,74 @@ class CuLLaVOModel(nn.Module):
             return (loss,) + out if loss is not None else out
         return CullavoCausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=None, hidden_states=hs_t,
                                              attentions=None)
+
+    # -- KV-cache inference (reference :605-636 and HF generate; generation.py) ------------------
+    def _forward_cached(self, input_ids, pixel_values, attention_mask, position_ids, cache, inputs_embeds,
+                        vision_feature_layer, strategy, labels, return_dict, max_len: int | None = None):
+        from .generation import lm_infer
+        if torch.is_grad_enabled() and any(p.requires_grad for ar in self.arenas.values() for p in ar.params.values()):
+            torch.set_grad_enabled(False)  # inference only, as under the reference's torch.inference_mode()
+            try:
+                return self._forward_cached(input_ids, pixel_values, attention_mask, position_ids, cache,
+                                            inputs_embeds, vision_feature_layer, strategy, labels, return_dict,
+                                            max_len)
+            finally:
+                torch.set_grad_enabled(True)
+        self.vision_tower.eval()
+        first = cache is None or cache.get_seq_length() == 0
+        if inputs_embeds is None:
+            inputs_embeds = self.get_input_embeddings()(input_ids)
+            if first and pixel_values is not None and input_ids.shape[1] != 1:
+                image_features = self._image_features(pixel_values, vision_feature_layer, strategy)
+                inputs_embeds, attention_mask, position_ids = self._merge(image_features, inputs_embeds, input_ids,
+                                                                          attention_mask)
+        B, L = inputs_embeds.shape[:2]
+        if max_len is None:
+            max_len = L + 256
+        logits, cache = lm_infer(self.language_model, inputs_embeds, attention_mask, position_ids, cache, max_len)
+        out = CullavoCausalLMOutputWithPast(loss=None, logits=logits, past_key_values=cache, hidden_states=None,
+                                            attentions=None)
+        return out if return_dict else out.to_tuple()
+
+    @torch.no_grad()
+    def generate(self, input_ids=None, pixel_values=None, attention_mask=None, max_new_tokens: int = 20,
+                 do_sample: bool = False, temperature: float = 1.0, top_k: int = 50, top_p: float = 1.0,
+                 eos_token_id: int | None = None, pad_token_id: int | None = None, use_cache: bool = True,
+                 generator=None, **kw):
+        """Decoder-only generate: returns [B, S + new] (prompt ids then sampled ids), stopping when
+        every sequence has produced eos_token_id (finished rows are padded with pad_token_id)."""
+        from .generation import sample_next
+        if not use_cache:
+            raise NotImplementedError("generate() runs on the KV cache (use_cache=True)")
+        cfg = self.config
+        pad = pad_token_id if pad_token_id is not None else cfg.pad_token_id
+        B, S = input_ids.shape
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        n_img = int((input_ids == cfg.image_token_index).sum(-1).max()) if pixel_values is not None else 0
+        L0 = S + n_img * (cfg.vision_config.num_patches - 1)
+        out = self._forward_cached(input_ids, pixel_values, attention_mask, None, None, None,
+                                   cfg.vision_feature_layer, cfg.vision_feature_select_strategy, None, True,
+                                   max_len=L0 + max_new_tokens)
+        cache = out.past_key_values
+        logits = out.logits[:, -1]
+        finished = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
+        new = []
+        for step in range(max_new_tokens):
+            tok = sample_next(logits, do_sample=do_sample, temperature=temperature, top_k=top_k, top_p=top_p,
+                              generator=generator)
+            tok = torch.where(finished, torch.full_like(tok, pad), tok)
+            new.append(tok)
+            if eos_token_id is not None:
+                finished |= tok == eos_token_id
+                if bool(finished.all()):
+                    break
+            if step + 1 == max_new_tokens:
+                break
+            out = self._forward_cached(tok[:, None], None, None, None, cache, None, cfg.vision_feature_layer,
+                                       cfg.vision_feature_select_strategy, None, True)
+            logits = out.logits[:, -1]
+        return torch.cat([input_ids, torch.stack(new, 1).to(input_ids.dtype)], 1)
 
     # -- pieces ---------------------------------------------------------------------------------
     def _image_features(self, pixel_values, layer: int, strategy: str):

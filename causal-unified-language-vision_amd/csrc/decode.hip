@@ -1,0 +1,165 @@
+// KV-cache decode for generate() (reference cullavo/arch_cullavo.py:
+// 605-636 and the HF generate() loop it drives, :341-395).
+//
+// The cache is preallocated per layer as K, V [B, Lmax, H*D] bf16 (token stride ld_tok, batch
+// stride ld_batch). Prefill writes the prompt's rotated keys and values with kv_append; each
+// decode step appends one token and runs attn_decode: one query row per (batch, head) against
+// keys [kv_start[b], kv_len[b]). Decode attention is HBM-bound (every cached key and value is
+// read once per step), so it is split over the keys (flash-decoding): workgroup (chunk, h, b)
+// scores 256 keys with 8 lanes per key (each lane 16 dims, coalesced 256 B rows), keeps the
+// chunk's max / sum / unnormalised P.V in f32 partials, and a combine kernel rescales and sums
+// the chunks in a fixed order (deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int kChunk = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+
+__global__ __launch_bounds__(256) void kv_append_k(const u16* __restrict__ ks, int64_t ldks, const u16* __restrict__ vs,
+                                                  int64_t ldvs, u16* __restrict__ kc, u16* __restrict__ vc,
+                                                  int64_t ld_tok, int64_t ld_b, const int32_t* __restrict__ start,
+                                                  int B, int Lnew, int64_t hd) {
+  const int64_t per_row = hd / 8, total = (int64_t)B * Lnew * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / per_row, c = (i % per_row) * 8;
+    const int b = (int)(row / Lnew), t = (int)(row % Lnew);
+    const int64_t dst = (int64_t)b * ld_b + (int64_t)(start[b] + t) * ld_tok + c;
+    *reinterpret_cast<u16x8*>(kc + dst) = *reinterpret_cast<const u16x8*>(ks + row * ldks + c);
+    *reinterpret_cast<u16x8*>(vc + dst) = *reinterpret_cast<const u16x8*>(vs + row * ldvs + c);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ Kc,
+                                                    const u16* __restrict__ Vc, int64_t ld_tok, int64_t ld_b,
+                                                    const int32_t* __restrict__ kv_len,
+                                                    const int32_t* __restrict__ kv_start, float scale_log2,
+                                                    float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                    int H, int nchunk) {
+  static_assert(D == 128, "decode attention is specialised for the LM head_dim");
+  const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int t = threadIdx.x;
+  const int len = kv_len[b], k_lo = kv_start ? kv_start[b] : 0;
+  const int kbeg = c * kChunk, kend = min(len, kbeg + kChunk);
+  __shared__ float qs[D];
+  __shared__ float ps[kChunk];
+  __shared__ float red[8];
+  __shared__ float oacc[2][D];
+  const int64_t pidx = ((int64_t)b * H + h) * nchunk + c;
+  if (kbeg >= kend) {  // chunk past this row's length: empty partial
+    if (t < D) part_o[pidx * D + t] = 0.f;
+    if (t == 0) { part_ml[2 * pidx] = -INFINITY; part_ml[2 * pidx + 1] = 0.f; }
+    return;
+  }
+  if (t < D) qs[t] = bf2f(Q[(int64_t)b * ldq + (int64_t)h * D + t]) * scale_log2;
+  __syncthreads();
+  const u16* Kb = Kc + (int64_t)b * ld_b + (int64_t)h * D;
+  const u16* Vb = Vc + (int64_t)b * ld_b + (int64_t)h * D;
+  // scores: 8 lanes per key (16 dims each), 32 keys per pass
+  const int sub = t & 7, slot = t >> 3;
+#pragma unroll 2
+  for (int pass = 0; pass < kChunk / 32; ++pass) {
+    const int key = kbeg + pass * 32 + slot;
+    const bool live = key < kend && key >= k_lo;
+    float acc = 0.f;
+    if (live) {
+      float kv[16];
+      const u16* kp = Kb + (int64_t)key * ld_tok + sub * 16;
+      load8(kp, kv);
+      load8(kp + 8, kv + 8);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc += qs[sub * 16 + j] * kv[j];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (sub == 0) ps[pass * 32 + slot] = live ? acc : -INFINITY;
+  }
+  __syncthreads();
+  // chunk max and sum
+  const int lane = t & 63, wv = t >> 6;
+  float s = ps[t];
+  float m = wave_max(s);
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float p = (s == -INFINITY) ? 0.f : exp2f(s - m);
+  __syncthreads();
+  ps[t] = p;
+  float l = wave_sum(p);
+  if (lane == 0) red[4 + wv] = l;
+  __syncthreads();
+  l = red[4] + red[5] + red[6] + red[7];
+  // P.V: thread owns dim d for every other key
+  const int d = t & (D - 1), half = t >> 7;
+  float o = 0.f;
+  for (int k = half; k < kend - kbeg; k += 2) o += ps[k] * bf2f(Vb[(int64_t)(kbeg + k) * ld_tok + d]);
+  oacc[half][d] = o;
+  __syncthreads();
+  if (t < D) part_o[pidx * D + t] = oacc[0][t] + oacc[1][t];
+  if (t == 0) { part_ml[2 * pidx] = m; part_ml[2 * pidx + 1] = l; }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void attn_decode_combine_k(const float* __restrict__ part_o,
+                                                          const float* __restrict__ part_ml, u16* __restrict__ O,
+                                                          int64_t ldo, int H, int nchunk) {
+  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const int64_t base = ((int64_t)b * H + h) * nchunk;
+  float M = -INFINITY;
+  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, part_ml[2 * (base + c)]);
+  float L = 0.f, acc = 0.f;
+  if (M != -INFINITY) {
+    for (int c = 0; c < nchunk; ++c) {
+      const float mc = part_ml[2 * (base + c)];
+      if (mc == -INFINITY) continue;
+      const float w = exp2f(mc - M);
+      L += w * part_ml[2 * (base + c) + 1];
+      acc += w * part_o[(base + c) * D + d];
+    }
+  }
+  O[(int64_t)b * ldo + (int64_t)h * D + d] = f2bf(L > 0.f ? acc / L : 0.f);  // no visible key -> 0
+}
+
+}  // namespace
+
+extern "C" int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, void* k_cache,
+                                 void* v_cache, int64_t ld_tok, int64_t ld_batch, const int32_t* start, int B,
+                                 int Lnew, int64_t hd, void* stream) {
+  CV_REQUIRE(hd % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ld_tok % 8 == 0 && ld_batch % 8 == 0, CULLAVO_EINVAL,
+             "kv_append: sizes and strides must be multiples of 8");
+  CV_REQUIRE(start != nullptr, CULLAVO_EINVAL, "kv_append: start positions");
+  if (B == 0 || Lnew == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int64_t work = (int64_t)B * Lnew * (hd / 8);
+  const int g = (int)std::min<int64_t>(cdiv(work, 256), 8192);
+  kv_append_k<<<g, 256, 0, s>>>((const u16*)k, ldk, (const u16*)v, ldv, (u16*)k_cache, (u16*)v_cache, ld_tok,
+                                ld_batch, start, B, Lnew, hd);
+  return cullavo_check_launch("kv_append");
+}
+
+extern "C" size_t cullavo_attn_decode_workspace(int B, int H, int max_len, int D) {
+  const int64_t nchunk = cdiv((int64_t)std::max(max_len, 1), kChunk);
+  return (size_t)B * H * nchunk * (D + 2) * sizeof(float);
+}
+
+extern "C" int cullavo_attn_decode(const void* q, int64_t ldq, const void* k_cache, const void* v_cache,
+                                   int64_t ld_tok, int64_t ld_batch, const int32_t* kv_len, const int32_t* kv_start,
+                                   void* o, int64_t ldo, int B, int H, int max_len, int D, float scale,
+                                   float* workspace, void* stream) {
+  CV_REQUIRE(D == 128, CULLAVO_EUNSUPPORTED, "decode attention: head_dim 128");
+  CV_REQUIRE(kv_len != nullptr && workspace != nullptr, CULLAVO_EINVAL, "decode attention: kv_len / workspace");
+  CV_REQUIRE(ld_tok >= (int64_t)H * D && ldq >= (int64_t)H * D && ldo >= (int64_t)H * D && ld_tok % 8 == 0,
+             CULLAVO_EINVAL, "decode attention: strides");
+  if (B == 0 || H == 0 || max_len <= 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int nchunk = (int)cdiv((int64_t)max_len, kChunk);
+  float* part_o = workspace;
+  float* part_ml = workspace + (int64_t)B * H * nchunk * D;
+  attn_decode_k<128><<<dim3(nchunk, H, B), 256, 0, s>>>((const u16*)q, ldq, (const u16*)k_cache,
+                                                        (const u16*)v_cache, ld_tok, ld_batch, kv_len, kv_start,
+                                                        scale * kLog2e, part_o, part_ml, H, nchunk);
+  attn_decode_combine_k<128><<<dim3(H, B), 128, 0, s>>>(part_o, part_ml, (u16*)o, ldo, H, nchunk);
+  return cullavo_check_launch("attn_decode");
+}

@@ -1,0 +1,138 @@
+"""KV-cache decode and generate().
+
+Reference: CuLLaVOModel.generate(**inputs, do_sample=True, temperature=0.9, top_k=50,
+top_p=0.95, max_new_tokens=1000, use_cache=True) (cullavo/arch_cullavo.py:362-363, the
+step-2 pre-labelling loop) runs HF's GenerationMixin over forward(); the cached branch of that
+forward is :605-636 (transformers ~4.37 llava: the new token's position is the number of
+attended tokens so far, position_ids = attention_mask.sum(-1) - 1).
+
+MI355X design: the cache is preallocated once per generate() call in HBM as K, V
+[layers, B, Lmax, H*D] bf16; the prompt (text + 576 image rows, merged exactly as training
+does) is prefilled through the same fused kernels (GEMMs, RoPE, causal flash attention) with
+its rotated keys/values appended by kv_append; every decode step runs the layers on one row
+per sequence and attends with the split-KV attn_decode kernel. Left-padded batches are
+supported through kv_start (keys before the first attended token are masked); a prompt with
+holes in its attention mask is not (decode attention reads one contiguous key range).
+Sampling (temperature, top-k, top-p, multinomial; or greedy) follows HF's warper order on the
+GPU with torch ops: it is O(B x vocab) per token and not a kernel of the hot path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .functions import StepContext
+
+
+class KVCache:
+    """Per-layer K, V [B, Lmax, H*D] in HBM plus the per-row state the decode kernels read."""
+
+    def __init__(self, n_layers: int, B: int, max_len: int, H: int, D: int, device, dtype=torch.bfloat16):
+        self.k = torch.empty((n_layers, B, max_len, H * D), dtype=dtype, device=device)
+        self.v = torch.empty_like(self.k)
+        self.B, self.max_len, self.H, self.D = B, max_len, H, D
+        self.length = 0                      # rows written (same for every sequence)
+        self.kv_start = None                 # int32 [B]: first attended key (left padding)
+        self.next_pos = None                 # int64 [B]: RoPE position of the next token
+
+    def __len__(self):
+        return self.k.shape[0]
+
+    def __getitem__(self, layer: int):
+        """HF legacy view: (key, value) as [B, H, L, D] over the filled rows."""
+        B, L, H, D = self.B, self.length, self.H, self.D
+        return (self.k[layer, :, :L].view(B, L, H, D).transpose(1, 2),
+                self.v[layer, :, :L].view(B, L, H, D).transpose(1, 2))
+
+    def get_seq_length(self) -> int:
+        return self.length
+
+
+def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int):
+    """One LlamaDecoderLayer over Lnew new rows per sequence (prefill: Lnew = prompt length on an
+    empty cache; decode: Lnew = 1), appending their keys/values to the cache. No autograd."""
+    cfg = layer.cfg
+    d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
+    lg = layer.lora_groups
+    B = sctx.B
+    x1, _ = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
+    t, _ = lg["qkv"].forward(x1, False, 0)
+    qkv = ops.linear(x1, layer.w_qkv(), addend=t)
+    q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+    ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
+    start = torch.full((B,), cache.length, dtype=torch.int32, device=h.device)
+    ops.kv_append(k, v, cache.k[li], cache.v[li], start, B=B, Lnew=Lnew)
+    if Lnew > 1:
+        o, _ = ops.attn_fwd(q, k, v, B=B, H=H, Lq=Lnew, Lk=Lnew, D=D, scale=D ** -0.5, causal=True,
+                            kv_start=sctx.kv_start)
+    else:
+        kv_len = torch.full((B,), cache.length + 1, dtype=torch.int32, device=h.device)
+        o = ops.attn_decode(q, cache.k[li], cache.v[li], kv_len, B=B, H=H, D=D, max_len=cache.length + 1,
+                            scale=D ** -0.5, kv_start=sctx.kv_start)
+    t, _ = lg["o"].forward(o, False, 0)
+    h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h, addend=t)
+    x2, _ = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
+    t, _ = lg["gu"].forward(x2, False, 0)
+    gu = ops.linear(x2, layer.w_gu(), addend=t)
+    a = ops.swiglu_fwd(gu)
+    t, _ = lg["down"].forward(a, False, 0)
+    return ops.linear(a, layer.mlp.down_proj.weight, residual=h2, addend=t)
+
+
+def lm_infer(lm, embeds, attention_mask, position_ids, cache: KVCache | None, max_len: int):
+    """LlamaForCausalLM with a KV cache: prefill (cache None or empty) or one decode step.
+    Returns (logits [B, Lnew, V] bf16, cache)."""
+    B, Lnew, d = embeds.shape
+    cfg = lm.cfg
+    if cache is None:
+        cache = KVCache(cfg.num_hidden_layers, B, max_len, cfg.num_attention_heads, cfg.head_dim, embeds.device)
+    if cache.length == 0:
+        if attention_mask is None:
+            attention_mask = torch.ones(B, Lnew, dtype=torch.long, device=embeds.device)
+        am = attention_mask.to(torch.int64)
+        first = (am.cumsum(-1) == 0).sum(-1)
+        # contiguous valid range only: zeros may appear only before the first attended token
+        holes = (am.sum(-1) + first != Lnew)
+        if bool(holes.any()):
+            raise NotImplementedError("KV-cache generation needs left padding (no masked tokens after the "
+                                      "first attended one)")
+        cache.kv_start = first.to(torch.int32)
+        if position_ids is None:
+            position_ids = (am.cumsum(-1) - 1).masked_fill(am == 0, 1)
+        cache.next_pos = position_ids[:, -1].to(torch.int64) + 1
+    else:
+        if Lnew != 1:
+            raise NotImplementedError("after the prefill, cached steps take one token per sequence")
+        if cache.length + 1 > cache.max_len:
+            raise ValueError(f"KV cache full ({cache.max_len} rows)")
+        if position_ids is None:
+            position_ids = cache.next_pos[:, None]
+        cache.next_pos = cache.next_pos + 1
+    sctx = StepContext(B, Lnew, position_ids, cache.kv_start, lora_seed=0)
+    h = embeds.reshape(B * Lnew, d).contiguous()
+    for li, layer in enumerate(lm.model.layers):
+        h = layer_infer(layer, h, sctx, cache, li, Lnew)
+    cache.length += Lnew
+    x, _ = ops.rmsnorm_fwd(h, lm.model.norm.weight, cfg.rms_norm_eps)
+    logits = ops.linear(x, lm.lm_head.weight)
+    return logits.view(B, Lnew, -1), cache
+
+
+def sample_next(logits, *, do_sample: bool, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                generator=None):
+    """HF's warper order (temperature -> top-k -> top-p) then multinomial; argmax when greedy."""
+    if not do_sample:
+        return logits.argmax(-1)
+    x = logits.float()
+    if temperature != 1.0:
+        x = x / temperature
+    if top_k and top_k > 0:
+        kth = torch.topk(x, min(top_k, x.shape[-1]), dim=-1).values[..., -1:]
+        x = x.masked_fill(x < kth, float("-inf"))
+    if top_p < 1.0:
+        sx, si = torch.sort(x, descending=False, dim=-1)
+        cum = sx.softmax(-1).cumsum(-1)
+        remove = cum <= (1 - top_p)
+        remove[..., -1:] = False
+        x = x.masked_fill(remove.scatter(-1, si, remove), float("-inf"))
+    return torch.multinomial(x.softmax(-1), 1, generator=generator).squeeze(-1)

@@ -434,10 +434,14 @@ class LlamaForCausalLM(nn.Module):
     def forward(self, input_ids=None, attention_mask=None, position_ids=None, past_key_values=None,
                 inputs_embeds=None, use_cache=None, output_attentions=None, output_hidden_states=None,
                 return_dict=None, **kw):
-        if past_key_values is not None or use_cache:
-            raise NotImplementedError("KV-cache decode is SURVEY.md §8(f) row 2 (not built yet)")
         if inputs_embeds is None:
             inputs_embeds = self.model.embed_tokens(input_ids)
+        if past_key_values is not None or use_cache:
+            from .generation import lm_infer
+            with torch.no_grad():
+                logits, cache = lm_infer(self, inputs_embeds, attention_mask, position_ids, past_key_values,
+                                         inputs_embeds.shape[1] + 256)
+            return CausalLMOutput(logits, past_key_values=cache)
         B, L, d = inputs_embeds.shape
         if position_ids is None:
             position_ids = torch.arange(L, device=inputs_embeds.device).expand(B, L)

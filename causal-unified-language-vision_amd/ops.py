@@ -18,7 +18,7 @@ __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "swiglu_fwd", "swiglu_bwd",
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
-    "ce_reduce", "ce_bwd", "adamw", "sumsq", "clip_coef", "scale_inplace",
+    "ce_reduce", "ce_bwd", "adamw", "sumsq", "clip_coef", "scale_inplace", "kv_append", "attn_decode",
 ]
 
 _DT = {torch.bfloat16: DT_BF16, torch.float32: DT_F32}
@@ -271,6 +271,26 @@ def attn_fwd(q, k, v, *, B: int, H: int, Lq: int, Lk: int, D: int, scale: float,
     call("attn_fwd", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(o), _ld(o), _ptr(lse), B, H, Lq, Lk,
          D, float(scale), int(causal), _ptr(kv_start), _dt(q), _stream())
     return o, lse
+
+
+def kv_append(k, v, k_cache, v_cache, start, *, B: int, Lnew: int):
+    """k, v: [B*Lnew, >=hd] row-strided views; caches [B, Lmax, hd]; start int32 [B]."""
+    _dev(k, v, k_cache, v_cache, start)
+    hd = k_cache.shape[-1]
+    call("kv_append", _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(k_cache), _ptr(v_cache), k_cache.stride(1),
+         k_cache.stride(0), _ptr(start), B, Lnew, hd, _stream())
+
+
+def attn_decode(q, k_cache, v_cache, kv_len, *, B: int, H: int, D: int, max_len: int, scale: float,
+                kv_start=None, out=None):
+    """One query row per batch (q [B, >=H*D]) against cache keys kv_start[b] <= j < kv_len[b]."""
+    _dev(q, k_cache, v_cache, kv_len, kv_start)
+    o = out if out is not None else torch.empty((B, H * D), dtype=q.dtype, device=q.device)
+    nbytes = lib().cullavo_attn_decode_workspace(B, H, max_len, D)
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+    call("attn_decode", _ptr(q), _ld(q), _ptr(k_cache), _ptr(v_cache), k_cache.stride(1), k_cache.stride(0),
+         _ptr(kv_len), _ptr(kv_start), _ptr(o), _ld(o), B, H, max_len, D, float(scale), _ptr(ws), _stream())
+    return o
 
 
 def attn_bwd(q, k, v, o, do, lse, *, B: int, H: int, Lq: int, Lk: int, D: int, scale: float, causal: bool,

@@ -182,6 +182,21 @@ int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                      float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
 
+/* ---- KV-cache decode (generate) --------------------------------------
+ * Cache per layer: K, V [B, Lmax, H*D] bf16, token stride ld_tok, batch stride ld_batch.
+ * kv_append copies Lnew new rows per batch (k/v: [B*Lnew, hd] with row strides) into cache
+ * rows start[b] .. start[b]+Lnew-1. attn_decode: one query row per batch (q [B, H*D], ldq)
+ * against cache keys kv_start[b] <= key < kv_len[b] (kv_start nullable); max_len >= every
+ * kv_len sizes the split over keys; workspace: cullavo_attn_decode_workspace bytes (f32).
+ * A row with no visible key returns zeros (as the training kernel's fully masked rows). */
+int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, void* k_cache, void* v_cache,
+                      int64_t ld_tok, int64_t ld_batch, const int32_t* start, int B, int Lnew, int64_t hd,
+                      void* stream);
+size_t cullavo_attn_decode_workspace(int B, int H, int max_len, int D);
+int cullavo_attn_decode(const void* q, int64_t ldq, const void* k_cache, const void* v_cache, int64_t ld_tok,
+                        int64_t ld_batch, const int32_t* kv_len, const int32_t* kv_start, void* o, int64_t ldo,
+                        int B, int H, int max_len, int D, float scale, float* workspace, void* stream);
+
 /* ---- embeddings / merge ------------------------------------------------------------------ */
 /* get_input_embeddings()(input_ids) (reference cullavo/arch_cullavo.py:582) */
 int cullavo_embedding_fwd(const int64_t* ids, int64_t n, const void* table, int64_t vocab,

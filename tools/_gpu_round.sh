@@ -1,5 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-for t in full lora; do
-timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu-baseline --trainable $t > gpurun_out/loss0_$t.log 2>&1 || exit 1
-done
+timeout -k 10 600 python -m pytest tests/test_generation.py -x -q -m gpu > gpurun_out/gen_tests.log 2>&1
+echo "rc=$?" >> gpurun_out/gen_tests.log
