@@ -6,14 +6,15 @@
 // decode step appends one token and runs attn_decode: one query row per (batch, head) against
 // keys [kv_start[b], kv_len[b]). Decode attention is HBM-bound (every cached key and value is
 // read once per step), so it is split over the keys (flash-decoding): workgroup (chunk, h, b)
-// scores 256 keys with 8 lanes per key (each lane 16 dims, coalesced 256 B rows), keeps the
+// scores 128 keys with 8 lanes per key (each lane 16 dims, coalesced 256 B rows, all loads in
+// flight before use), forms P.V with 16 dim-groups x 16 key-groups of 16 B loads, keeps the
 // chunk's max / sum / unnormalised P.V in f32 partials, and a combine kernel rescales and sums
 // the chunks in a fixed order (deterministic).
 #include "common.h"
 
 namespace {
 
-constexpr int kChunk = 256;
+constexpr int kChunk = 128;
 constexpr float kLog2e = 1.4426950408889634f;
 
 __global__ __launch_bounds__(256) void kv_append_k(const u16* __restrict__ ks, int64_t ldks, const u16* __restrict__ vs,
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
   __shared__ float qs[D];
   __shared__ float ps[kChunk];
   __shared__ float red[8];
-  __shared__ float oacc[2][D];
+  __shared__ float oacc[16][D];
   const int64_t pidx = ((int64_t)b * H + h) * nchunk + c;
   if (kbeg >= kend) {  // chunk past this row's length: empty partial
     if (t < D) part_o[pidx * D + t] = 0.f;
@@ -56,48 +57,73 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
   __syncthreads();
   const u16* Kb = Kc + (int64_t)b * ld_b + (int64_t)h * D;
   const u16* Vb = Vc + (int64_t)b * ld_b + (int64_t)h * D;
-  // scores: 8 lanes per key (16 dims each), 32 keys per pass
+  // scores: 8 lanes per key (16 dims each, one 256 B row per key), 32 keys per pass; all the
+  // passes' loads are issued before any is consumed
   const int sub = t & 7, slot = t >> 3;
-#pragma unroll 2
-  for (int pass = 0; pass < kChunk / 32; ++pass) {
-    const int key = kbeg + pass * 32 + slot;
-    const bool live = key < kend && key >= k_lo;
-    float acc = 0.f;
-    if (live) {
-      float kv[16];
-      const u16* kp = Kb + (int64_t)key * ld_tok + sub * 16;
-      load8(kp, kv);
-      load8(kp + 8, kv + 8);
+  constexpr int kPass = kChunk / 32;
+  u16x8 kr[kPass][2];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc += qs[sub * 16 + j] * kv[j];
-    }
+  for (int pass = 0; pass < kPass; ++pass) {
+    const int key = min(kbeg + pass * 32 + slot, kend - 1);
+    const u16* kp = Kb + (int64_t)key * ld_tok + sub * 16;
+    kr[pass][0] = *reinterpret_cast<const u16x8*>(kp);
+    kr[pass][1] = *reinterpret_cast<const u16x8*>(kp + 8);
+  }
+  float qv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) qv[j] = qs[sub * 16 + j];
+#pragma unroll
+  for (int pass = 0; pass < kPass; ++pass) {
+    const int key = kbeg + pass * 32 + slot;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += qv[j] * bf2f(kr[pass][0][j]) + qv[8 + j] * bf2f(kr[pass][1][j]);
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     acc += __shfl_xor(acc, 4);
-    if (sub == 0) ps[pass * 32 + slot] = live ? acc : -INFINITY;
+    if (sub == 0) ps[pass * 32 + slot] = (key < kend && key >= k_lo) ? acc : -INFINITY;
   }
   __syncthreads();
-  // chunk max and sum
+  // chunk max and sum (kChunk = 128 scores, threads >= 128 carry -inf / 0)
   const int lane = t & 63, wv = t >> 6;
-  float s = ps[t];
+  const float s = t < kChunk ? ps[t] : -INFINITY;
   float m = wave_max(s);
   if (lane == 0) red[wv] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const float p = (s == -INFINITY) ? 0.f : exp2f(s - m);
   __syncthreads();
-  ps[t] = p;
+  if (t < kChunk) ps[t] = p;
   float l = wave_sum(p);
   if (lane == 0) red[4 + wv] = l;
   __syncthreads();
   l = red[4] + red[5] + red[6] + red[7];
-  // P.V: thread owns dim d for every other key
-  const int d = t & (D - 1), half = t >> 7;
-  float o = 0.f;
-  for (int k = half; k < kend - kbeg; k += 2) o += ps[k] * bf2f(Vb[(int64_t)(kbeg + k) * ld_tok + d]);
-  oacc[half][d] = o;
+  // P.V: thread (dim group dg of 8 dims, key group kg) sums keys kg, kg+16, ...
+  const int dg = t & 15, kg = t >> 4;
+  const int nk = kend - kbeg;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u16x8 vr[kChunk / 16];
+#pragma unroll
+  for (int i = 0; i < kChunk / 16; ++i) {
+    const int k = min(kg + 16 * i, nk - 1);
+    vr[i] = *reinterpret_cast<const u16x8*>(Vb + (int64_t)(kbeg + k) * ld_tok + dg * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < kChunk / 16; ++i) {
+    const int k = kg + 16 * i;
+    const float pk = k < nk ? ps[k] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] += pk * bf2f(vr[i][j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) oacc[kg][dg * 8 + j] = o[j];
   __syncthreads();
-  if (t < D) part_o[pidx * D + t] = oacc[0][t] + oacc[1][t];
+  if (t < D) {
+    float sum = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) sum += oacc[g][t];
+    part_o[pidx * D + t] = sum;
+  }
   if (t == 0) { part_ml[2 * pidx] = m; part_ml[2 * pidx + 1] = l; }
 }
 

@@ -790,7 +790,7 @@ int launch8p(GemmArgs p, hipStream_t s) {
 // features) are cut into K chunks of >= 4 K-tiles, enough of them for ~512 workgroups.
 int splitk_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
   const int64_t tiles = cdiv(M, BM) * cdiv(N, BN), nk = cdiv(K, BK);
-  if (tiles >= 192 || nk < 8) return 1;
+  if (tiles >= 384 || nk < 8) return 1;
   int64_t s = std::min<int64_t>(std::max<int64_t>(512 / tiles, 2), std::min<int64_t>(nk / 4, 32));
   if (s < 2) return 1;
   const int64_t per = cdiv(nk, s);

@@ -48,7 +48,7 @@ class KVCache:
         return self.length
 
 
-def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int):
+def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int, start, kv_len):
     """One LlamaDecoderLayer over Lnew new rows per sequence (prefill: Lnew = prompt length on an
     empty cache; decode: Lnew = 1), appending their keys/values to the cache. No autograd."""
     cfg = layer.cfg
@@ -60,13 +60,11 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int)
     qkv = ops.linear(x1, layer.w_qkv(), addend=t)
     q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
     ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
-    start = torch.full((B,), cache.length, dtype=torch.int32, device=h.device)
     ops.kv_append(k, v, cache.k[li], cache.v[li], start, B=B, Lnew=Lnew)
     if Lnew > 1:
         o, _ = ops.attn_fwd(q, k, v, B=B, H=H, Lq=Lnew, Lk=Lnew, D=D, scale=D ** -0.5, causal=True,
                             kv_start=sctx.kv_start)
     else:
-        kv_len = torch.full((B,), cache.length + 1, dtype=torch.int32, device=h.device)
         o = ops.attn_decode(q, cache.k[li], cache.v[li], kv_len, B=B, H=H, D=D, max_len=cache.length + 1,
                             scale=D ** -0.5, kv_start=sctx.kv_start)
     t, _ = lg["o"].forward(o, False, 0)
@@ -110,8 +108,10 @@ def lm_infer(lm, embeds, attention_mask, position_ids, cache: KVCache | None, ma
         cache.next_pos = cache.next_pos + 1
     sctx = StepContext(B, Lnew, position_ids, cache.kv_start, lora_seed=0)
     h = embeds.reshape(B * Lnew, d).contiguous()
+    start = torch.full((B,), cache.length, dtype=torch.int32, device=h.device)
+    kv_len = start + Lnew
     for li, layer in enumerate(lm.model.layers):
-        h = layer_infer(layer, h, sctx, cache, li, Lnew)
+        h = layer_infer(layer, h, sctx, cache, li, Lnew, start, kv_len)
     cache.length += Lnew
     x, _ = ops.rmsnorm_fwd(h, lm.model.norm.weight, cfg.rms_norm_eps)
     logits = ops.linear(x, lm.lm_head.weight)

@@ -104,6 +104,7 @@ class GemmDesc(ctypes.Structure):
 
 
 DROP_NONE, DROP_A, DROP_B, DROP_OUT = 0, 1, 2, 3
+SMALL_M = 256  # Linear calls with at most this many rows (KV-cache decode) may run split-K
 
 
 def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
@@ -144,9 +145,12 @@ def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: 
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
     pre = torch.empty((M, N), dtype=x.dtype, device=x.device) if want_preact else None
     ldr = _ld(residual) if residual is not None else 0
-    if addend is None:
+    if addend is None and M > SMALL_M:
         gemm(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
              residual=residual, ldr=ldr)
+    elif addend is None:  # decode-sized rows: let the library split K over the idle CUs
+        gemm_ex(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
+                residual=residual, ldr=ldr)
     else:
         if addend.shape != (M, N):
             raise ValueError(f"linear: addend {tuple(addend.shape)} != {(M, N)}")
