@@ -466,9 +466,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
 
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE;
-      const int64_t k1 = (int64_t)(kt + 1) * BK;
+    const bool more = kt + 1 < nk;
+    char* nxt = smem + ((kt + 1) & 1) * STAGE;
+    const int64_t k1 = (int64_t)(kt + 1) * BK;
+    // next K-tile's LDS-DMA pieces, all issued before this tile's MFMAs (issuing them one by
+    // one between MFMA groups measured 5-15 % slower, profiles/r01/gemm_8phase.md)
+    if (more) {
       dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, k1, p.K, nxt, wave, lane);
       dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
     }

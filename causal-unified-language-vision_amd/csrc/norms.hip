@@ -113,6 +113,115 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
   }
 }
 
+// RMSNorm backward, production form: 8-wave workgroups (two per CU) over contiguous row chunks,
+// two waves per row, the row's x, dy and dres loads issued together, dw accumulated per wave in
+// registers and folded per workgroup through LDS in slot order (deterministic) into ONE partial
+// row per workgroup (<= 512 partial rows).
+constexpr int kBwd8Blocks = 512;
+
+// 8 raw elements kept in their storage type until used (register budget of 8-wave blocks)
+template <typename T> struct Raw8;
+template <> struct Raw8<u16> {
+  u16x8 v;
+  DEV void load(const u16* p) { v = *reinterpret_cast<const u16x8*>(p); }
+  DEV float operator[](int j) const { return bf2f(v[j]); }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  DEV void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  DEV float operator[](int j) const { return j < 4 ? a[j] : b[j - 4]; }
+};
+
+template <typename T, int NCH, bool WANT_DW, bool HAS_DRES>
+__global__ __launch_bounds__(512, WANT_DW ? 2 : 4) void rmsnorm_bwd8_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                         const T* __restrict__ w, const float* __restrict__ rstd,
+                                                         T* __restrict__ dx, const T* __restrict__ dres,
+                                                         float* __restrict__ part, int64_t rows, int cols,
+                                                         int64_t rows_per_block) {
+  // two waves per row (wave = 2*slot + half; half h owns the 512-column chunks c = h, h+2, ...),
+  // four rows in flight per workgroup, the row's dot product combined through LDS
+  constexpr int NH = (NCH + 1) / 2;  // chunks per half
+  extern __shared__ float sdw[];     // [cols] when WANT_DW
+  __shared__ float pdot[2][4][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = wave >> 1, half = wave & 1;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float acc[NH][8];
+#pragma unroll
+  for (int c = 0; c < NH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  const int iters = (int)cdiv(r1 - r0, (int64_t)4);
+  for (int it = 0; it < iters; ++it) {
+    const int64_t row = r0 + 4 * it + slot;
+    const bool live = row < r1;
+    const float r = live ? rstd[row] : 0.f;
+    Raw8<T> xr[NH], dr[NH], rr[NH];
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (2 * c + half) * 512 + lane * 8;
+      if (live && 2 * c + half < NCH && col < cols) {
+        xr[c].load(x + row * cols + col);
+        dr[c].load(dy + row * cols + col);
+        if (HAS_DRES) rr[c].load(dres + row * cols + col);
+      }
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (2 * c + half) * 512 + lane * 8;
+      if (live && 2 * c + half < NCH && col < cols) {
+        Raw8<T> wr;
+        wr.load(w + col);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = xr[c][j] * r;
+          dot += dr[c][j] * wr[j] * xh;
+          if (WANT_DW) acc[c][j] += dr[c][j] * Elt<T>::rnd(xh);
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) pdot[it & 1][slot][half] = dot;
+    __syncthreads();
+    dot = (pdot[it & 1][slot][0] + pdot[it & 1][slot][1]) / (float)cols;
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (2 * c + half) * 512 + lane * 8;
+      if (live && 2 * c + half < NCH && col < cols) {
+        Raw8<T> wr;
+        wr.load(w + col);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = r * (dr[c][j] * wr[j] - xr[c][j] * r * dot);
+          if (HAS_DRES) o[j] += rr[c][j];
+        }
+        store8(dx + row * cols + col, o);
+      }
+    }
+  }
+  if (WANT_DW) {  // fold the four row slots in order; the two halves own disjoint columns
+    for (int sl = 0; sl < 4; ++sl) {
+      if (slot == sl) {
+#pragma unroll
+        for (int c = 0; c < NH; ++c) {
+          const int col = (2 * c + half) * 512 + lane * 8;
+          if (2 * c + half < NCH && col < cols)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sdw[col + j] = (sl == 0 ? 0.f : sdw[col + j]) + acc[c][j];
+        }
+      }
+      __syncthreads();
+    }
+    for (int col = threadIdx.x; col < cols; col += 512) part[(int64_t)blockIdx.x * cols + col] = sdw[col];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 template <typename T, int NCH>
 __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -243,20 +352,22 @@ __global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy,
 }
 
 // partial [nslots, cols] f32 -> out[c] = beta*out[c] + sum_p part[p][c]
-// block = 64 columns x 4 slot groups (coalesced 256 B row segments), fixed summation order
+// block = 64 columns x 16 slot groups (coalesced 256 B row segments), fixed summation order
 template <typename TO>
-__global__ __launch_bounds__(256) void reduce_partials_k(const float* __restrict__ part, int nslots,
-                                                         int cols, TO* __restrict__ out, float beta) {
-  __shared__ float red[4][64];
+__global__ __launch_bounds__(1024) void reduce_partials_k(const float* __restrict__ part, int nslots,
+                                                          int cols, TO* __restrict__ out, float beta) {
+  __shared__ float red[16][64];
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + c;
   float s = 0.f;
   if (col < cols)
-    for (int p = g; p < nslots; p += 4) s += part[(int64_t)p * cols + col];
+    for (int p = g; p < nslots; p += 16) s += part[(int64_t)p * cols + col];
   red[g][c] = s;
   __syncthreads();
   if (g == 0 && col < cols) {
-    s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][c];
     if (beta != 0.f) s += beta * Elt<TO>::ld(out, col);
     Elt<TO>::st(out, col, s);
   }
@@ -281,7 +392,7 @@ int nch_for(int64_t cols) {
 
 template <typename TO>
 void launch_reduce(const float* part, int nslots, int cols, void* out, float beta, hipStream_t s) {
-  reduce_partials_k<TO><<<cdiv(cols, 64), 256, 0, s>>>(part, nslots, cols, (TO*)out, beta);
+  reduce_partials_k<TO><<<cdiv(cols, 64), 1024, 0, s>>>(part, nslots, cols, (TO*)out, beta);
 }
 
 int bwd_blocks(int64_t rows) { return (int)std::min<int64_t>(kBwdBlocks, cdiv(rows, kRowsPerBlock)); }
@@ -317,10 +428,15 @@ extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w,
   CV_REQUIRE(dw == nullptr || ws != nullptr, CULLAVO_EINVAL, "dw requires a workspace");
   if (rows == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
-  const int nb = bwd_blocks(rows);
   const int nch = nch_for(cols);
   const bool want = dw != nullptr, hr = dres != nullptr;
-#define RMB(T, WD, HR) NCH_DISPATCH(nch, rmsnorm_bwd_k<T, NC, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols))
+  const bool wide = nch > 8;  // 8192 columns: the 4-wave kernel (register budget)
+  const int nb = wide ? bwd_blocks(rows) : (int)std::min<int64_t>(kBwd8Blocks, cdiv(rows, 4));
+  const int64_t rpb = cdiv(rows, nb);
+  const size_t lds = want ? (size_t)cols * sizeof(float) : 0;
+#define RMB(T, WD, HR)                                                                                        \
+  if (wide) rmsnorm_bwd_k<T, 16, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols); \
+  else NCH_DISPATCH(nch, rmsnorm_bwd8_k<T, (NC > 8 ? 8 : NC), WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb))
   if (dtype == CULLAVO_DT_BF16) {
     if (want && hr) { RMB(u16, true, true); } else if (want) { RMB(u16, true, false); }
     else if (hr) { RMB(u16, false, true); } else { RMB(u16, false, false); }
@@ -332,7 +448,7 @@ extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w,
   }
 #undef RMB
   if (want) {
-    const int nslots = nb * kRowsPerBlock;
+    const int nslots = wide ? nb * kRowsPerBlock : nb;
     if (w_dtype == CULLAVO_DT_BF16) launch_reduce<u16>(ws, nslots, (int)cols, dw, beta, s);
     else launch_reduce<float>(ws, nslots, (int)cols, dw, beta, s);
   }
