@@ -24,6 +24,7 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr int kVmcnt0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 
 // LDS image of a [rows][D] bf16 tile, 16-byte chunk ch of row r. D=128: the dual-use XOR
 // image (conflict-free for both the row reads and the tr16 reads, cdna_hip_programming.md
@@ -146,6 +147,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     sk.store(bufK(0));
     sv.store(bufV(0));
   }
+  // vmcnt(0) the compiler can see on every path: the Q fragments are then known to have
+  // landed inside the loop, so the in-loop prefetch of the next K/V tile is not waited for
+  // before the first MFMA (hipcc otherwise emits vmcnt(0) there: the prefetch is conditional)
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);
   __syncthreads();
 
   for (int t = t0; t < ntiles; ++t) {
@@ -332,6 +337,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
     sdo.store(smem + TILE);
     stage_aux(smem, qt0);
   }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
   __syncthreads();
 
   for (int qt = qt0; block_live && qt < nqt; ++qt) {
@@ -456,6 +462,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
     sk.store(bufK(0));
     sv.store(bufV(0));
   }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
   __syncthreads();
   for (int t = t0; t < ntiles; ++t) {
     const int cur = (t - t0) & 1;

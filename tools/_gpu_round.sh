@@ -1,10 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_ops_gpu.py -x -q -k "gemm or linear or rmsnorm or layernorm" > gpurun_out/gemm_tests.log 2>&1 || exit 1
-timeout -k 10 300 python -m pytest tests/test_model_gpu.py -x -q > gpurun_out/model_tests.log 2>&1 || exit 1
-timeout -k 10 120 python tools/norm_bench.py > gpurun_out/norm_bench.log 2>&1 || exit 2
-rm -f gpurun_out/spread.log
-for sp in 0 1 0 1; do
-  echo "== spread $sp" >> gpurun_out/spread.log
-  CULLAVO_GEMM_SPREAD=$sp timeout -k 10 300 python tools/gemm_bench.py --modes 2,3 --iters 10 >> gpurun_out/spread.log 2>&1 || exit 3
-done
+timeout -k 10 600 python -m pytest tests/test_ops_gpu.py -x -q > gpurun_out/ops_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -m pytest tests/test_model_gpu.py tests/test_generation.py -x -q > gpurun_out/model_tests.log 2>&1 || exit 1
+timeout -k 10 200 python tools/attn_bench.py > gpurun_out/attn_bench.log 2>&1 || exit 2
+timeout -k 10 400 python bench.py --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/bench_full.log 2>&1 || exit 3
+echo "== before (previous attention build)" >> gpurun_out/attn_bench.log
+cp causal-unified-language-vision_amd/libcullavo_hip.so /tmp/lib_after.so && cp causal-unified-language-vision_amd/build/lib_before.so causal-unified-language-vision_amd/libcullavo_hip.so && timeout -k 10 200 python tools/attn_bench.py >> gpurun_out/attn_bench.log 2>&1
+cp /tmp/lib_after.so causal-unified-language-vision_amd/libcullavo_hip.so

@@ -1,0 +1,36 @@
+"""Flash attention forward / backward at the production shapes (HIP-event timing):
+LM causal D=128 (B=8, L=1088, H=32) and CLIP non-causal D=64 (B=64, T=577, H=16).
+Algorithmic FLOPs: fwd 4*B*H*Lq*Lk*D (x1/2 causal), bwd 2.5x fwd."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cullavo_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=10):
+    for _ in range(2):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("ViT D64", 64, 577, 16, 64, False)]:
+    qkv = (torch.randn(B * L, 3 * H * D, device="cuda") * 0.5).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o, lse = ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal)
+    do = torch.randn_like(o)
+    dqkv = torch.empty_like(qkv)
+    fl = 4.0 * B * H * L * L * D * (0.5 if causal else 1.0)
+    tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
+    tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
+                                     causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
+                                     dv=dqkv[:, 2 * H * D:]))
+    print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd {tb * 1e3:8.1f} us {2.5 * fl / tb / 1e9:7.1f} TF")
