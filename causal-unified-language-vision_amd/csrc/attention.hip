@@ -26,6 +26,10 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kVmcnt0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 
+// bare v_exp_f32: results below 2^-126 flush to zero (softmax weights that small are noise);
+// exp2f adds a denormal range fix-up (compare, select, ldexp) around every call
+DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // LDS image of a [rows][D] bf16 tile, 16-byte chunk ch of row r. D=128: the dual-use XOR
 // image (conflict-free for both the row reads and the tr16 reads, cdna_hip_programming.md
 // T10 (b)); D=64: chunk ^ ((r>>1)&7) (row reads conflict-free, tr reads 2-way).
@@ -169,32 +173,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
       for (int s = 0; s < NS; ++s)
         st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufK(cur), kt * 32, s, lane), qf[s], st[kt], 0, 0, 0);
     }
-    // scale, mask, tile max
-    float tmax = -INFINITY;
+    // mask (boundary tiles only, branch-free), tile max on the raw scores (c > 0)
     const int kbase = t * KT;
     const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
+    if (need_mask) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kbase + kt * 32 + acc_row(r, hf);
+          const bool dead = key >= Lk || key < kstart || (CAUSAL && key > q);
+          st[kt][r] = dead ? -INFINITY : st[kt][r];
+        }
+    }
+    float tmax = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = st[kt][r] * c;
-        if (need_mask) {
-          const int key = kbase + kt * 32 + acc_row(r, hf);
-          if (key >= Lk || key < kstart || (CAUSAL && key > q)) v = -INFINITY;
-        }
-        st[kt][r] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[kt][r]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
     const float mnew = fmaxf(m, tmax);
     const float muse = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = exp2f(m - muse);
+    const float alpha = fast_exp2(m - muse);
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(st[kt][r] - muse);
+        const float pv = fast_exp2(fmaf(st[kt][r], c, -muse));  // exp2(-inf) = 0 for masked keys
         st[kt][r] = pv;
         rs += pv;
       }
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
       for (int j = 0; j < 4; ++j) {
         const int r = rr * 4 + j;
         const int qq = qt * QT + 8 * rr + 4 * hf + j;
-        float pv = exp2f(sacc[r] * c - l4[j] * kLog2e);
+        float pv = fast_exp2(fmaf(sacc[r], c, -l4[j] * kLog2e));
         if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
         sacc[r] = pv;
         pacc[r] = pv * (pacc[r] - d4[j]);
@@ -481,7 +487,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = kbase + acc_row(r, hf);
-      float pv = exp2f(st[r] * c - lse2);
+      float pv = fast_exp2(fmaf(st[r], c, -lse2));
       if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
       dpt[r] = pv * (dpt[r] - del);
     }
