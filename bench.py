@@ -128,8 +128,8 @@ def gemm_kernel_name(M, N, K):
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
     tile = _lib.lib().cullavo_gemm_plan(M, N, K, 0, 0, ctypes.byref(g))
-    names = {0: "gemm_k<0, 0, 1>", 1: "gemm256_k<0, 0, 1, 256, 128>", 2: "gemm256_k<0, 0, 1, 256, 256>",
-             3: "gemm256_k<0, 0, 1, 192, 256>"}
+    names = {0: "gemm_k<0, 0, 1>", 1: "gemm256_k<0, 0, 1, 256, 128>", 2: "gemm256_k<0, 0, 1, 256, 256, 1>",
+             3: "gemm256_k<0, 0, 1, 192, 256, 1>"}
     return names[tile], int(g.value)
 
 

@@ -42,6 +42,7 @@ struct GemmArgs {
   uint64_t drop_seed;
   float* part;        // split-K: f32 partials [gridDim.y][M][N] (register-staged kernel only)
   int kt_per;         // K-tiles per split
+  int epi_lds;        // 8-wave kernels: LDS-staged 16-B epilogue (all pointers 16-B aligned)
 };
 
 // ---- LDS images -----------------------------------------------------------------------------
@@ -207,6 +208,116 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
       for (int j = 0; j < 4; ++j) o[j] = v[j];
     }
     *reinterpret_cast<f32x4*>(cp) = o;
+  }
+}
+
+// the same epilogue for 8 consecutive columns C[m][n .. n+7] with 16-B accesses (the
+// LDS-staged path below; every pointer 16-B aligned and every ld a multiple of 8, see
+// lds_epi_ok)
+template <int CT>
+DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
+  if (m >= p.M || n >= p.N) return;  // N % 8 == 0: the whole group is in range
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = a[j] * p.alpha;
+  if (p.drop_mode == 3) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = drop_keep(p.drop_seed, p.drop_thr, m, n + j) ? v[j] * p.drop_scale : 0.f;
+  }
+  if (p.bias) {
+    const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bf2f(bv[j]);
+  }
+  if (p.addend) {
+    const u16x8 av = *reinterpret_cast<const u16x8*>(p.addend + m * p.ld_add + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) + bf2f(av[j]);
+  }
+  if (p.act != CULLAVO_ACT_NONE || p.preact) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]);
+    if (p.preact) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+      *reinterpret_cast<u16x8*>(p.preact + m * p.ldc + n) = o;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
+  }
+  if (p.residual) {
+    const u16x8 rv = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
+  }
+  if (CT == CULLAVO_DT_BF16) {
+    u16* cp = (u16*)p.C + m * p.ldc + n;
+    if (p.beta != 0.f) {
+      const u16x8 old = *reinterpret_cast<const u16x8*>(cp);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += p.beta * bf2f(old[j]);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+    *reinterpret_cast<u16x8*>(cp) = o;
+  } else {
+    float* cp = (float*)p.C + m * p.ldc + n;
+    f32x4 o0, o1;
+    if (p.beta != 0.f) {
+      const f32x4 q0 = *reinterpret_cast<const f32x4*>(cp), q1 = *reinterpret_cast<const f32x4*>(cp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o0[j] = v[j] + p.beta * q0[j]; o1[j] = v[4 + j] + p.beta * q1[j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o0[j] = v[j]; o1[j] = v[4 + j]; }
+    }
+    *reinterpret_cast<f32x4*>(cp) = o0;
+    *reinterpret_cast<f32x4*>(cp + 4) = o1;
+  }
+}
+
+// LDS-staged epilogue of the 8-wave kernels (256-column tiles): per row half (wave row wm),
+// the owning waves write their f32 accumulators into a [BM/2][256] image (16-B chunk c of row
+// r at chunk c ^ (r & 15): conflict-free ds_write_b128), then all 512 threads run store8 on
+// 8 contiguous columns each, so every global access is a full-width 16-B access and 32 lanes
+// cover one 512-B output row (the per-lane 8-B stores of the MFMA layout touch 16 rows per
+// instruction; measured +3-4 % on the whole GEMM, tools/lab/gemm_lab.hip).
+template <int CT, int BM2, int TMW, int TN>
+DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wm,
+                      int wn, int lane) {
+  static_assert(TN == 4, "256-column tiles");
+  constexpr int R = BM2 / 2;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int r = tm * 16 + (lane & 15);
+          const int c = wn * 16 + tn * 4 + (lane >> 4);
+          *reinterpret_cast<f32x4*>(smem + r * 1024 + ((c ^ (r & 15)) << 4)) = acc[tm][tn];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R * 32 / 512; ++i) {
+      const int idx = threadIdx.x + 512 * i;
+      const int r = idx >> 5, pr = idx & 31;
+      const int sw = (pr >> 3) & 1;  // odd chunk first for pairs 8-15, 24-31: conflict-free reads
+      const int c0 = 2 * pr + sw, c1 = 2 * pr + 1 - sw;
+      const char* rowp = smem + r * 1024;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(rowp + ((c0 ^ (r & 15)) << 4));
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(rowp + ((c1 ^ (r & 15)) << 4));
+      const f32x4 lo = sw ? x1 : x0, hi = sw ? x0 : x1;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+      store8<CT>(p, v, m0 + half * R + r, n0 + pr * 8);
+    }
+    __syncthreads();
   }
 }
 
@@ -421,7 +532,11 @@ DEV frag8 read_frag_w(const char* lds, int rbase, int ks, int lane) {
   return __builtin_bit_cast(frag8, v);
 }
 
-template <int AL, int BL, int CT, int BMT, int BN>
+// LDR selects which waves stage the next K-tile: 0 = all eight (each wave issues its share of
+// LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
+// 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
+// partner wave's MFMAs instead of beside nothing).
+template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
 __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
   constexpr int TILE_A = BM2 * BK * 2;
@@ -472,8 +587,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
     // next K-tile's LDS-DMA pieces, all issued before this tile's MFMAs (issuing them one by
     // one between MFMA groups measured 5-15 % slower, profiles/r01/gemm_8phase.md)
     if (more) {
-      dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, k1, p.K, nxt, wave, lane);
-      dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
+      if constexpr (LDR == 0) {
+        dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, k1, p.K, nxt, wave, lane);
+        dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
+      } else {
+        const bool loader = LDR == 1 ? wave < 4 : wave >= 4;
+        if (loader) {
+          const int lw = wave & 3;
+          dma_tile<AL, BM2, 4>(ra, p.lda, m0, p.M, k1, p.K, nxt, lw, lane);
+          dma_tile<BL, BN, 4>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, lw, lane);
+        }
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -505,6 +629,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
     __syncthreads();
   }
 
+  if constexpr (BN == 256) {
+    if (p.epi_lds) {
+      lds_epilogue<CT, BM2, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
+      return;
+    }
+  }
 #pragma unroll
   for (int tm = 0; tm < TMW; ++tm) {
     const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
@@ -823,26 +953,44 @@ int launch(const GemmArgs& p, hipStream_t s) {
   return cullavo_check_launch("gemm");
 }
 
-template <int AL, int BL, int CT, int BM2, int BN2>
+template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0>
 int launch256(GemmArgs p, hipStream_t s) {
   const int smem = 2 * (BM2 * BK * 2 + BN2 * BK * 2);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2>,
+    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
   p.tiles_m = (int)cdiv(p.M, BM2);
   p.tiles_n = (int)cdiv(p.N, BN2);
-  gemm256_k<AL, BL, CT, BM2, BN2><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
   return cullavo_check_launch("gemm256");
+}
+
+// Which waves stage the next K-tile, per operand layout (tools/gemm_bench.py, same-run A/B on
+// the model's shapes): with a K-contiguous A one loader wave per SIMD wins 7-14 % (forward and
+// dX products); with both operands read transposed (dW) all eight waves loading wins 10-15 %.
+template <int AL, int BL>
+constexpr int default_ldr() { return AL == 0 ? 1 : 0; }
+
+// tile modes 6 / 7: the 256x256 / 192x256 kernels with the other loader choice (A/B testing)
+template <int AL, int BL>
+int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
+  constexpr int L = 1 - default_ldr<AL, BL>();
+  if constexpr (AL == 0) {
+    if (tile == 7)
+      return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256, L>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256, L>(p, s);
+  }
+  return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256, L>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256, L>(p, s);
 }
 
 // Kernel-shape choice. Time model = FLOPs / (per-tile rate of the shape) x (whole rounds of
 // tiles over the 256 CUs / exact rounds): the 8-wave kernels run one 512-thread block per CU,
 // so a grid of 544 tiles takes 3 rounds for 2.125 rounds of work. Per-tile rates (TFLOP/s,
-// measured on MI355X with tools/gemm_bench.py): 256x256 ~1250, 192x256
-// ~1190 (A K-contiguous only), 128x128 4-wave (2 blocks/CU, 512 slots) ~840.
+// measured on MI355X with tools/gemm_bench.py): 256x256 ~1300, 192x256
+// ~1150 (A K-contiguous only; the 256-row tile reads 14 % less LDS per MFMA), 128x128 4-wave
+// (2 blocks/CU, 512 slots) ~840.
 // kT8p / kT8p10 (the ping-pong kernel) are selectable but not auto-chosen: measured against
 // the 2-stage kernels on the model's shapes (tools/gemm_bench.py, several boxes) they win
 // 3-7 % on big-N forward products (q|k|v, lm_head), lose 10-25 % on dX, dW and N = 4096,
@@ -853,8 +1001,8 @@ enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
-  const C cands[3] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, 1250.0},
-                      {kT192x256, 192, 256, 256, 1190.0}};
+  const C cands[3] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, 1300.0},
+                      {kT192x256, 192, 256, 256, 1150.0}};
   double best = 1e300;
   int bid = kT128;
   for (const C& c : cands) {
@@ -874,17 +1022,27 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 }  // namespace
 
 static int g_force_tile = -1;
+static int g_epi_lds = 1;
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = (mode >= 0 && mode <= 5) ? mode : -1;
+  g_force_tile = (mode >= 0 && mode <= 7) ? mode : -1;
+  return prev;
+}
+
+// A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
+extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
+  const int prev = g_epi_lds;
+  g_epi_lds = lds_staged ? 1 : 0;
   return prev;
 }
 
 extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid) {
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
-  static const int bm[6] = {128, 256, 256, 192, 256, 256}, bn[6] = {128, 128, 256, 256, 256, 256};
+  if (tile == 7 && a_layout != 0) tile = 6;
+  static const int bm[8] = {128, 256, 256, 192, 256, 256, 256, 192};
+  static const int bn[8] = {128, 128, 256, 256, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -931,6 +1089,11 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.part = nullptr;
   p.kt_per = 0;
   {
+    auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+    p.epi_lds = a16(d.C) && a16(d.bias) && a16(d.preact) && a16(residual) && a16(d.addend) &&
+                (d.addend == nullptr || d.ld_addend % 8 == 0) && g_epi_lds;
+  }
+  {
     int per = 0;
     const int splits = splitk_plan(M, N, K, &per);
     const int64_t need = (int64_t)splits * M * N * 4;
@@ -962,10 +1125,16 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     L8P(1, 1)
 #undef L8P
   }
+  if (tile >= 6) {
+    if (a_layout == 0 && b_layout == 0) return launch_alt_ldr<0, 0>(p, tile, f32, s);
+    if (a_layout == 0 && b_layout == 1) return launch_alt_ldr<0, 1>(p, tile, f32, s);
+    if (a_layout == 1 && b_layout == 0) return launch_alt_ldr<1, 0>(p, tile, f32, s);
+    return launch_alt_ldr<1, 1>(p, tile, f32, s);
+  }
   if (tile != kT128) {
-#define L256(AL, BL)                                                                                         \
-  if (tile == kT256x256) return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256>(p, s); \
-  if (tile == kT192x256 && AL == 0) return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256>(p, s); \
+#define L256(AL, BL)                                                                                       \
+  if (tile == kT256x256) return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256, default_ldr<AL, BL>()>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256, default_ldr<AL, BL>()>(p, s); \
+  if (tile == kT192x256 && AL == 0) return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256, default_ldr<0, BL>()>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256, default_ldr<0, BL>()>(p, s); \
   return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 128>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 128>(p, s);
     if (a_layout == 0 && b_layout == 0) { L256(0, 0) }
     if (a_layout == 0 && b_layout == 1) { L256(0, 1) }

@@ -112,9 +112,14 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
  * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
  * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel
- * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers).
+ * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
+ * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
+/* Tuning/A-B switch: 1 (default) = the 8-wave kernels stage their epilogue through LDS and
+   store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
+   Returns the previous setting. */
+int cullavo_gemm_set_epilogue(int lds_staged);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls. */
 int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid);

@@ -43,7 +43,8 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, -1], ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "auto"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, -1],
+                ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "t256alt", "t192alt", "auto"])
 def tile_mode(request):
     from cullavo_amd import _lib
     prev = _lib.lib().cullavo_gemm_set_tile(request.param)
@@ -66,8 +67,16 @@ def test_gemm_layouts(M, N, K, al, bl, tile_mode):
     close(C, ref, 8e-3, f"gemm {al}{bl} {M}x{N}x{K}")
 
 
+@pytest.fixture(params=[1, 0], ids=["lds_epi", "lane_epi"])
+def epi_mode(request):
+    from cullavo_amd import _lib
+    prev = _lib.lib().cullavo_gemm_set_epilogue(request.param)
+    yield request.param
+    _lib.lib().cullavo_gemm_set_epilogue(prev)
+
+
 @pytest.mark.parametrize("act", [0, 1, 2])
-def test_gemm_epilogues(act, tile_mode):
+def test_gemm_epilogues(act, tile_mode, epi_mode):
     M, N, K = 300, 264, 192
     x, w, b = rnd((M, K), 3), rnd((N, K), 4, 0.1), rnd((N,), 5, 0.1)
     r = rnd((M, N), 6)
@@ -76,6 +85,27 @@ def test_gemm_epilogues(act, tile_mode):
     a = {0: p, 1: F.gelu(p), 2: O.quick_gelu(p)}[act]
     close(pre, p, 8e-3, "preact")
     close(y, a.to(BF).float() + r.float(), 8e-3, "epilogue")
+
+
+def test_gemm_epilogue_paths_bit_identical(tile_mode):
+    """The LDS-staged 16-B epilogue and the per-lane one compute the same roundings in the same
+    order, so every output (bias, LoRA addend, residual, preact, accumulate) is bit-identical."""
+    from cullavo_amd import _lib
+    M, N, K = 520, 776, 320
+    x, w, b = rnd((M, K), 31).to(DEV), rnd((N, K), 32, 0.1).to(DEV), rnd((N,), 33, 0.1).to(DEV)
+    r, t = rnd((M, N), 34).to(DEV), rnd((M, N), 35, 0.05).to(DEV)
+    outs = []
+    for epi in (1, 0):
+        prev = _lib.lib().cullavo_gemm_set_epilogue(epi)
+        try:
+            y, pre = ops().linear(x, w, b, act=ops().ACT_GELU, residual=r, want_preact=True, addend=t)
+            acc = rnd((N, K), 36, dtype=torch.float32).to(DEV)
+            ops().linear_dw(y, x, acc, beta=1.0)
+            outs.append((y, pre, acc))
+        finally:
+            _lib.lib().cullavo_gemm_set_epilogue(prev)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
 
 
 def test_gemm_f32_accumulate_beta(tile_mode):
@@ -114,7 +144,7 @@ def test_gemm_pipelined_repeatable(al, bl):
     back to back at sizes with K tails and several K-tiles, must be bit-identical every time
     (a read racing its LDS-DMA shows up as rare wrong tiles) and match the fp32 product."""
     from cullavo_amd import _lib
-    for mode in (2, 4, 5):
+    for mode in (2, 3, 4, 5, 6, 7):
         prev = _lib.lib().cullavo_gemm_set_tile(mode)
         try:
             for (M, N, K) in [(768, 1024, 4160), (520, 264, 200), (2048, 2048, 1024)]:

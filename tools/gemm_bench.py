@@ -51,13 +51,16 @@ def main():
             r = ref[kind]()
             tb = timeit(ref[kind], a.iters)
             line = f"{name:8s} {kind:3s} T={T} out={out_f} in={in_f}  hipBLASLt {fl / tb / 1e9:7.1f} TF"
-            for mode in [int(m) for m in a.modes.split(",")]:
-                lib.cullavo_gemm_set_tile(mode)
+            for mode in [m.strip() for m in a.modes.split(",")]:
+                lane_epi = mode.endswith("L")  # e.g. "-1L": same kernel, per-lane epilogue
+                lib.cullavo_gemm_set_tile(int(mode.rstrip("L")))
+                lib.cullavo_gemm_set_epilogue(0 if lane_epi else 1)
                 o = ours[kind]()
                 err = ((o.float() - r.float()).norm() / r.float().norm()).item()
                 t = timeit(ours[kind], a.iters)
-                line += f" | m{mode:+d} {fl / t / 1e9:7.1f} TF err {err:.1e}"
+                line += f" | m{mode} {fl / t / 1e9:7.1f} TF err {err:.1e}"
             lib.cullavo_gemm_set_tile(-1)
+            lib.cullavo_gemm_set_epilogue(1)
             print(line, flush=True)
 
 
