@@ -23,6 +23,12 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
+
+// bijective XCD-aware block remap (as in gemm.hip; cdna_hip_programming.md §5)
+DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kVmcnt0 = 0x0F70;  // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 
@@ -112,9 +118,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   constexpr int ND = D / 32;             // O^T tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;  // heavy causal blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
+  // 1-D grid of (query block, head, batch), XCD-remapped: the query blocks of one (b, h) run
+  // on one XCD and share its K/V tiles in L2; heavy causal blocks first within a group
+  const int nqb = (Lq + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
   const int q = qb * 128 + wave * 32 + (lane & 31);
   const int kstart = kv_start ? kv_start[b] : 0;
@@ -278,14 +288,14 @@ __global__ __launch_bounds__(256) void attn_delta_k(const u16* __restrict__ O, i
 // 32-row query tiles staged in LDS. S = Q K^T and dP = dO V^T keep the key on the lane;
 // dV = P^T dO and dK = dS^T Q take P / dS straight from the accumulators (A operand) and
 // dO / Q as transposed LDS fragments.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int QT>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
     const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
     const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
     const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
     int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
     const int32_t* __restrict__ kv_start) {
-  constexpr int QT = 32;
+  constexpr int NSUB = QT / 32;  // 32-row query sub-tiles per barrier
   constexpr int TILE = QT * D * 2;
   constexpr int NS = D / 16;
   constexpr int ND = D / 32;
@@ -293,10 +303,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
   // [buf][Q tile | dO tile | lse(32 f32) | delta(32 f32)]
   constexpr int BUF = 2 * TILE + 2 * QT * 4;
 
-  const int nkb = gridDim.x;
-  const int kb = CAUSAL ? blockIdx.x : blockIdx.x;
-  (void)nkb;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // 1-D grid of (key block, head, batch), XCD-remapped: the key blocks of one (b, h) share
+  // its Q / dO tiles in one XCD's L2
+  const int nkb = (Lk + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, hb = lid / nkb;
+  const int h = hb % H, b = hb / H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
   const int key = kb * 128 + wave * 32 + (lane & 31);  // this lane's key (operand column)
   const int kstart = kv_start ? kv_start[b] : 0;
@@ -327,21 +339,25 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
   const bool block_live = kmin < Lk && (kmin + 128 > kstart);
 
   Stage<QT, D> sq, sdo;
-  auto stage_aux = [&](char* buf, int qt) {  // lse / delta for 32 rows (threads 0..63)
-    if (threadIdx.x < 64) {
-      const int r = threadIdx.x & 31;
-      const int qq = qt * QT + r;
-      float* dst = (float*)(buf + 2 * TILE) + (threadIdx.x >> 5) * QT + r;
-      const float val = (threadIdx.x < 32) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
-      *dst = val;
+  // lse / delta of a query tile (threads 0..2QT-1, one value each): loaded together with the
+  // tile's Q / dO prefetch and written to LDS with them (not loaded and waited for at the end)
+  float aux = 0.f;
+  auto load_aux = [&](int qt) {
+    if (threadIdx.x < 2 * QT) {
+      const int qq = qt * QT + (int)threadIdx.x % QT;
+      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
     }
+  };
+  auto store_aux = [&](char* buf) {
+    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TILE))[threadIdx.x] = aux;
   };
   if (block_live && qt0 < nqt) {
     sq.load(Qb, ldq, qt0 * QT, Lq);
     sdo.load(dOb, lddo, qt0 * QT, Lq);
     sq.store(smem);
     sdo.store(smem + TILE);
-    stage_aux(smem, qt0);
+    load_aux(qt0);
+    store_aux(smem);
   }
   __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
   __syncthreads();
@@ -354,46 +370,56 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
     if (more) {
       sq.load(Qb, ldq, (qt + 1) * QT, Lq);
       sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+      load_aux(qt + 1);
     }
     const float* slse = (const float*)(buf + 2 * TILE);
     const float* sdel = slse + QT;
-    // S[q][key], dP[q][key]
-    f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+    // S[q][key], dP[q][key] of the NSUB 32-row sub-tiles (independent MFMA chains)
+    f32x16 sacc[NSUB], pacc[NSUB];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 0, s, lane), kf[s], sacc, 0, 0, 0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TILE, 0, s, lane), vf[s], pacc, 0, 0, 0);
-    }
+    for (int u = 0; u < NSUB; ++u) { sacc[u] = f32x16(0.f); pacc[u] = f32x16(0.f); }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u) {
+        sacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 32 * u, s, lane), kf[s], sacc[u], 0, 0, 0);
+        pacc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TILE, 32 * u, s, lane), vf[s], pacc[u], 0, 0, 0);
+      }
     // P = exp(S*scale - lse), dS = P * (dP - delta)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 8 * rr + 4 * hf);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 8 * rr + 4 * hf);
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = rr * 4 + j;
-        const int qq = qt * QT + 8 * rr + 4 * hf + j;
-        float pv = fast_exp2(fmaf(sacc[r], c, -l4[j] * kLog2e));
-        if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
-        sacc[r] = pv;
-        pacc[r] = pv * (pacc[r] - d4[j]);
+      for (int rr = 0; rr < 4; ++rr) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 32 * u + 8 * rr + 4 * hf);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 32 * u + 8 * rr + 4 * hf);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = rr * 4 + j;
+          const int qq = qt * QT + 32 * u + 8 * rr + 4 * hf + j;
+          float pv = fast_exp2(fmaf(sacc[u][r], c, -l4[j] * kLog2e));
+          if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
+          sacc[u][r] = pv;
+          pacc[u][r] = pv * (pacc[u][r] - d4[j]);
+        }
       }
-    }
-    // dV += P^T dO ; dK += dS^T Q   (A operand = accumulator, B = transposed LDS fragment)
+    // dV += P^T dO ; dK += dS^T Q   (A operand = accumulator, B = transposed LDS fragment);
+    // sub-tile order = the 32-row tile order, so every QT sums in the same order
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const frag8 pf = pack_frag(sacc, s);
-      const frag8 df = pack_frag(pacc, s);
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) {
-        dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TILE, 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
-        dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_frag<D>(buf, 16 * s, dt * 32, lane), dk[dt], 0, 0, 0);
+      for (int s = 0; s < 2; ++s) {
+        const frag8 pf = pack_frag(sacc[u], s);
+        const frag8 df = pack_frag(pacc[u], s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TILE, 32 * u + 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_frag<D>(buf, 32 * u + 16 * s, dt * 32, lane), dk[dt], 0, 0, 0);
+        }
       }
-    }
     if (more) {
       sq.store(nbuf);
       sdo.store(nbuf + TILE);
-      stage_aux(nbuf, qt + 1);
+      store_aux(nbuf);
     }
     __syncthreads();
   }
@@ -415,21 +441,23 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
 // Kernel B: dQ. A wave owns 32 query rows (Q, dO fragments in registers, lse/delta per
 // lane); the workgroup sweeps 32-key K/V tiles. S^T = K Q^T, dP^T = V dO^T (query on the
 // lane), dQ^T += K^T dS^T with K^T as a transposed LDS fragment.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int KT>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
     const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
     const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
     const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dQ,
     int64_t lddq, int H, int Lq, int Lk, float scale, const int32_t* __restrict__ kv_start) {
-  constexpr int KT = 32;
   constexpr int TILE = KT * D * 2;
+  constexpr int NSUB = KT / 32;  // 32-key sub-tiles per barrier
   constexpr int NS = D / 16;
   constexpr int ND = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int nqb = gridDim.x;
-  const int qb = CAUSAL ? (nqb - 1 - blockIdx.x) : blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int nqb = (Lq + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // as attn_fwd_k: one (b, h) per XCD range
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
   const int q = qb * 128 + wave * 32 + (lane & 31);
   const int kstart = kv_start ? kv_start[b] : 0;
@@ -477,27 +505,35 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
       sk.load(Kb, ldk, (t + 1) * KT, Lk);
       sv.load(Vb, ldv, (t + 1) * KT, Lk);
     }
-    f32x16 st = f32x16(0.f), dpt = f32x16(0.f);
+    f32x16 st[NSUB], dpt[NSUB];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufK(cur), 0, s, lane), qf[s], st, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufV(cur), 0, s, lane), of[s], dpt, 0, 0, 0);
-    }
+    for (int u = 0; u < NSUB; ++u) { st[u] = f32x16(0.f); dpt[u] = f32x16(0.f); }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u) {
+        st[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufK(cur), 32 * u, s, lane), qf[s], st[u], 0, 0, 0);
+        dpt[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bufV(cur), 32 * u, s, lane), of[s], dpt[u], 0, 0, 0);
+      }
     const int kbase = t * KT;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kbase + acc_row(r, hf);
-      float pv = fast_exp2(fmaf(st[r], c, -lse2));
-      if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
-      dpt[r] = pv * (dpt[r] - del);
-    }
+    for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const frag8 df = pack_frag(dpt, s);
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * u + acc_row(r, hf);
+        float pv = fast_exp2(fmaf(st[u][r], c, -lse2));
+        if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
+        dpt[u][r] = pv * (dpt[u][r] - del);
+      }
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bufK(cur), 16 * s, dt * 32, lane), df, dq[dt], 0, 0, 0);
-    }
+    for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const frag8 df = pack_frag(dpt[u], s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+          dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bufK(cur), 32 * u + 16 * s, dt * 32, lane), df, dq[dt], 0, 0, 0);
+      }
     if (more) {
       sk.store(bufK(cur ^ 1));
       sv.store(bufV(cur ^ 1));
@@ -530,36 +566,47 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
   const int smem = 4 * 64 * D * 2;
   static bool once = false;
   if (!once) { set_smem(attn_fwd_k<D, CAUSAL>, smem); once = true; }
-  dim3 grid((unsigned)cdiv(Lq, 128), H, B);
+  const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
   attn_fwd_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_fwd");
 }
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int QT, int KT>
 int bwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
                int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
                u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
                const int32_t* ks, hipStream_t s) {
   const int64_t rows = (int64_t)B * Lq * H;
   attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
-  const int smem_a = 2 * (2 * 32 * D * 2 + 2 * 32 * 4);
-  const int smem_b = 4 * 32 * D * 2;
+  const int smem_a = 2 * (2 * QT * D * 2 + 2 * QT * 4);
+  const int smem_b = 4 * KT * D * 2;
   static bool once = false;
   if (!once) {
-    set_smem(attn_bwd_dkdv_k<D, CAUSAL>, smem_a);
-    set_smem(attn_bwd_dq_k<D, CAUSAL>, smem_b);
+    set_smem(attn_bwd_dkdv_k<D, CAUSAL, QT>, smem_a);
+    set_smem(attn_bwd_dq_k<D, CAUSAL, KT>, smem_b);
     once = true;
   }
-  dim3 ga((unsigned)cdiv(Lk, 128), H, B);
-  attn_bwd_dkdv_k<D, CAUSAL><<<ga, 256, smem_a, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk,
+  const unsigned ga = (unsigned)(cdiv(Lk, 128) * H * B);
+  attn_bwd_dkdv_k<D, CAUSAL, QT><<<ga, 256, smem_a, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk,
                                                       dv, lddv, H, Lq, Lk, scale, ks);
-  dim3 gb((unsigned)cdiv(Lq, 128), H, B);
-  attn_bwd_dq_k<D, CAUSAL><<<gb, 256, smem_b, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H,
+  const unsigned gb = (unsigned)(cdiv(Lq, 128) * H * B);
+  attn_bwd_dq_k<D, CAUSAL, KT><<<gb, 256, smem_b, s>>>(q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H,
                                                     Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
+// backward tile shape (cullavo_attn_set_bwd_tiles): bit 0 -> 64 query rows per dK/dV
+// barrier, bit 1 -> 64 keys per dQ barrier (else 32); -1 = per head dim, from the MI355X
+// sweep in tools/attn_bench.py: D=128 causal 64/32 (730 vs 746 us), D=64 32/64 (636 vs 646 us)
+int g_bwd_tiles = -1;
+
 }  // namespace
+
+extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
+  const int prev = g_bwd_tiles;
+  if (mode >= -1 && mode <= 3) g_bwd_tiles = mode;
+  return prev;
+}
 
 extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                 int64_t ldv, void* o, int64_t ldo, float* lse, int B, int H, int Lq, int Lk,
@@ -597,8 +644,12 @@ extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64
   hipStream_t s = CV_STREAM(stream);
   const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v, *O = (const u16*)o, *dO = (const u16*)dout;
   u16 *dQ = (u16*)dq, *dK = (u16*)dk, *dV = (u16*)dv;
-#define BWD(DD, CC) bwd_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+#define BWD4(DD, CC, QQ, KK) bwd_launch<DD, CC, QQ, KK>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+  const int tiles = g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 1 : 2);
+#define BWD(DD, CC) (tiles == 3 ? BWD4(DD, CC, 64, 64) : tiles == 2 ? BWD4(DD, CC, 32, 64) \
+                     : tiles == 1 ? BWD4(DD, CC, 64, 32) : BWD4(DD, CC, 32, 32))
   if (D == 128) return causal ? BWD(128, true) : BWD(128, false);
   return causal ? BWD(64, true) : BWD(64, false);
 #undef BWD
+#undef BWD4
 }

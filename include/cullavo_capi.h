@@ -186,6 +186,12 @@ int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                      int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                      float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
+/* Tuning/A-B switch for cullavo_attn_bwd's tile shape: bit 0 = 64 query rows per dK/dV
+   barrier, bit 1 = 64 keys per dQ barrier (else 32). Results are bitwise identical across
+   modes (same products summed in the same order). -1 (the default) picks per head dim
+   (D=128: 64/32, D=64: 32/64). Out-of-range values leave the mode unchanged. Returns the
+   previous mode. */
+int cullavo_attn_set_bwd_tiles(int mode);
 
 /* ---- KV-cache decode (generate) --------------------------------------
  * Cache per layer: K, V [B, Lmax, H*D] bf16, token stride ld_tok, batch stride ld_batch.

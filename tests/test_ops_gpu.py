@@ -305,6 +305,29 @@ def test_attention_fwd_bwd(B, H, L, D, causal):
     close(dq, tr(qf.grad), 2e-2, "dq")
 
 
+@pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
+def test_attention_bwd_tile_modes_bitwise(D, causal):
+    """Every backward tile shape (cullavo_attn_set_bwd_tiles) sums the same products in the same
+    order, so dQ/dK/dV agree bit for bit; ragged L and a left-padded batch row included."""
+    from cullavo_amd import _lib
+    B, H, L = 2, 3, 200
+    q, k, v, do = (rnd((B * L, H * D), s).to(DEV) for s in (91, 92, 93, 94))
+    ks = torch.tensor([0, 45], dtype=torch.int32, device=DEV)
+    kw = dict(B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal, kv_start=ks)
+    o, lse = ops().attn_fwd(q, k, v, **kw)
+    prev = _lib.lib().cullavo_attn_set_bwd_tiles(0)
+    try:
+        outs = []
+        for mode in range(4):
+            _lib.lib().cullavo_attn_set_bwd_tiles(mode)
+            outs.append([t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)])
+    finally:
+        _lib.lib().cullavo_attn_set_bwd_tiles(prev)
+    for mode in range(1, 4):
+        for name, a, b in zip("qkv", outs[0], outs[mode]):
+            assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode {mode}"
+
+
 def test_attention_strided_and_kv_start():
     B, H, L, D = 2, 2, 160, 128
     qkv = rnd((B * L, 3 * H * D), 80)

@@ -7,7 +7,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cullavo_amd import ops  # noqa: E402
+from cullavo_amd import _lib, ops  # noqa: E402
 
 
 def timeit(fn, iters=10):
@@ -30,7 +30,12 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
     dqkv = torch.empty_like(qkv)
     fl = 4.0 * B * H * L * L * D * (0.5 if causal else 1.0)
     tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
-    tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
-                                     causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
-                                     dv=dqkv[:, 2 * H * D:]))
-    print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd {tb * 1e3:8.1f} us {2.5 * fl / tb / 1e9:7.1f} TF")
+    res = []
+    for mode in range(4):
+        _lib.lib().cullavo_attn_set_bwd_tiles(mode)
+        tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
+                                         causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
+                                         dv=dqkv[:, 2 * H * D:]))
+        res.append(f"m{mode} {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.1f} TF")
+    _lib.lib().cullavo_attn_set_bwd_tiles(-1)
+    print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd " + " | ".join(res))
