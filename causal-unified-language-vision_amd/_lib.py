@@ -19,6 +19,7 @@ _CTYPE = {
     "int": ctypes.c_int,
     "int64_t": ctypes.c_int64,
     "float": ctypes.c_float,
+    "double": ctypes.c_double,
     "size_t": ctypes.c_size_t,
 }
 

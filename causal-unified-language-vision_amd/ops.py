@@ -19,6 +19,7 @@ __all__ = [
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
     "ce_reduce", "ce_bwd", "adamw", "sumsq", "clip_coef", "scale_inplace", "kv_append", "attn_decode",
+    "clip_image_preprocess",
 ]
 
 _DT = {torch.bfloat16: DT_BF16, torch.float32: DT_F32}
@@ -428,3 +429,21 @@ def clip_coef(sumsq_buf, max_norm: float, coef, norm_out=None):
 
 def scale_inplace(x, scale):
     call("scale_inplace", _ptr(x), x.numel(), _ptr(scale), _dt(x), _stream())
+
+
+# ---- image preprocessing (data step) -----------------------------------------------------------
+def clip_image_preprocess(images, Hr, Wr, h_bounds, h_kk, h_ksize, v_bounds, v_kk, v_ksize, top, left, crop_h,
+                          crop_w, rescale, mean, std, tmp, out):
+    """uint8 [B, C, H, W] (any strides) -> out [B, C, crop_h, crop_w]: PIL-bicubic resize to
+    (Hr, Wr) with the given Pillow coefficient tables, crop at (top, left), rescale, normalise"""
+    _dev(images, h_bounds, h_kk, v_bounds, v_kk, tmp, out)
+    B, C, H, W = images.shape
+    if not out.is_contiguous() or tuple(out.shape) != (B, C, crop_h, crop_w):
+        raise ValueError("out must be a contiguous [B, C, crop_h, crop_w] tensor")
+    if tmp.numel() < B * C * H * crop_w:
+        raise ValueError("tmp too small")
+    sb, sc, sy, sx = images.stride()
+    call("clip_image_preprocess", _ptr(images), B, C, H, W, sb, sc, sy, sx, Hr, Wr, _ptr(h_bounds), _ptr(h_kk),
+         int(h_ksize), _ptr(v_bounds), _ptr(v_kk), int(v_ksize), top, left, crop_h, crop_w, float(rescale),
+         *[float(m) for m in mean], *[float(s) for s in std], _ptr(tmp), _ptr(out), _dt(out), _stream())
+    return out

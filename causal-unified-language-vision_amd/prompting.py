@@ -1,0 +1,250 @@
+"""The data step: lbk.json records -> prompts, labels and pixel_values.
+
+Drop-ins for the reference's prompt builders and the processor call they end in:
+
+* ``make_system_prompt`` / ``make_and_add_prompt_and_label`` — reference
+  cullavo/arch_cullavo.py:28-61 (same signatures; the label of the system prompt covers the 575
+  extra image slots the merge inserts).
+* ``step2_process`` / ``eval_process`` — reference :397-543 / :63-94, for conversation records.
+  Records carrying ``boxes`` need detectron2's Visualizer to draw the boxes into the image
+  (:438-452); that drawing is out of scope here and raises NotImplementedError.
+* ``CuLLaVOProcessor`` — the LlavaProcessor call ``processor(text=..., images=..., padding=True,
+  return_tensors="pt")``: the caller's tokenizer (any object with HF's ``__call__`` /
+  ``pad_token_id`` / ``padding_side``; the real llava tokenizer is not available offline) pads
+  the text, and ``ClipImageProcessorHIP`` turns the uint8 images into pixel_values on the GPU
+  (csrc/imageprep.hip: PIL-bicubic shortest-edge resize, center crop, rescale, normalise,
+  bit-identical to transformers' CLIPImageProcessor).
+* ``load_lbk_records`` — reference datasets/registration/register_lbkllava_datasets.py:25-73
+  (``lbk.json`` ShareGPT4V conversations; image records kept only when the file exists).
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import ops
+
+SYSTEM_PROMPT = ("A chat between a curious human and an artificial intelligence assistant. "
+                 "The assistant gives helpful, detailed, and polite answers to the human's questions. ")
+OPENAI_CLIP_MEAN = (0.48145466, 0.4578275, 0.40821073)
+OPENAI_CLIP_STD = (0.26862954, 0.26130258, 0.27577711)
+N_IMAGE_SLOTS = 576
+
+
+def _token_ids(tokenizer, text: str, add_special_tokens: bool) -> torch.Tensor:
+    return tokenizer(text, return_tensors="pt", add_special_tokens=add_special_tokens).input_ids[0]
+
+
+def make_system_prompt(processor, device, ignore_index):
+    """reference cullavo/arch_cullavo.py:29-40"""
+    prompt = SYSTEM_PROMPT + "<image>"
+    length = _token_ids(processor.tokenizer, prompt, True).shape[0]
+    label = torch.full((length + N_IMAGE_SLOTS - 1,), ignore_index, dtype=torch.long, device=device)
+    return prompt, label
+
+
+def make_and_add_prompt_and_label(cullavo_prompt, cullavo_label, prompt, answer, processor, device, ignore_index):
+    """reference cullavo/arch_cullavo.py:42-61: the ' USER: ... ASSISTANT:' tokens are masked,
+    the answer and its '</s>' are supervised"""
+    prompt = " USER: " + prompt + " ASSISTANT:"
+    length = _token_ids(processor.tokenizer, prompt, False).shape[0]
+    prompt = prompt + " " + str(answer) + "</s>"
+    label_ids = _token_ids(processor.tokenizer, prompt, False).clone().long()
+    label_ids[:length] = ignore_index
+    label = torch.cat([torch.as_tensor(cullavo_label, dtype=torch.long).cpu(), label_ids]).to(device)
+    return cullavo_prompt + prompt, label
+
+
+def list2string(_list) -> str:
+    """reference cullavo/utils/utils.py:69-75"""
+    return ", ".join(str(x) for x in _list)
+
+
+def box2string(box) -> str:
+    """reference cullavo/utils/utils.py:77-83: '[x0, y0, x1, y1]' with 3 decimals"""
+    return "[" + ", ".join(f"{round(float(x), 3):.3f}" for x in box) + "]"
+
+
+# ---- images ------------------------------------------------------------------------------------
+def resize_output_size(H: int, W: int, shortest_edge: int):
+    """transformers get_resize_output_image_size(default_to_square=False) -> (h, w)"""
+    short, long = (W, H) if W <= H else (H, W)
+    new_short, new_long = shortest_edge, int(shortest_edge * long / short)
+    return (new_long, new_short) if W <= H else (new_short, new_long)
+
+
+class ClipImageProcessorHIP:
+    """CLIPImageProcessor (llava-1.5 / CLIP-L/14-336 settings) on the GPU.
+
+    __call__(images) takes uint8 images — a [B, C, H, W] tensor (the reference stacks CHW
+    tensors, cullavo/arch_cullavo.py:313,516), a [C, H, W] tensor, or a list of them with
+    different sizes — and returns pixel_values [B, C, crop, crop] (f32 by default, like the
+    processor; bf16 on request for the vision tower)."""
+
+    def __init__(self, shortest_edge: int = 336, crop_size: int = 336, rescale_factor: float = 1 / 255,
+                 image_mean=OPENAI_CLIP_MEAN, image_std=OPENAI_CLIP_STD, device=None):
+        self.shortest_edge = int(shortest_edge)
+        self.crop = (int(crop_size), int(crop_size))
+        self.rescale_factor = float(rescale_factor)
+        self.mean = tuple(float(np.float32(m)) for m in image_mean)
+        self.std = tuple(float(np.float32(s)) for s in image_std)
+        self.device = device
+        self._tables = {}
+
+    def _coeffs(self, in_size: int, out_size: int, device):
+        key = (in_size, out_size, str(device))
+        if key not in self._tables:
+            L = ops.lib()
+            ksize = L.cullavo_resample_coeffs(in_size, out_size, None, None, 0)
+            bounds = np.zeros(2 * out_size, np.int32)
+            kk = np.zeros(out_size * ksize, np.int32)
+            rc = L.cullavo_resample_coeffs(in_size, out_size, bounds.ctypes.data, kk.ctypes.data, ksize)
+            if rc != ksize:
+                raise ValueError(f"cullavo_resample_coeffs({in_size}, {out_size}) failed ({rc})")
+            self._tables[key] = (torch.from_numpy(bounds).to(device), torch.from_numpy(kk).to(device), ksize)
+        return self._tables[key]
+
+    def preprocess_batch(self, images: torch.Tensor, out_dtype=torch.float32, out=None) -> torch.Tensor:
+        """images: uint8 [B, C, H, W] on the GPU (any strides) -> pixel_values [B, C, ch, cw]"""
+        if images.dtype != torch.uint8 or images.dim() != 4:
+            raise ValueError("images must be a uint8 [B, C, H, W] tensor")
+        B, C, H, W = images.shape
+        if C > 3:
+            raise ValueError(f"expected at most 3 channels, got {C}")
+        dev = images.device
+        Hr, Wr = resize_output_size(H, W, self.shortest_edge)
+        ch, cw = self.crop
+        if ch > Hr or cw > Wr:
+            raise ValueError(f"crop {self.crop} larger than the resized image {(Hr, Wr)}")
+        top, left = (Hr - ch) // 2, (Wr - cw) // 2
+        hb, hk, hks = self._coeffs(W, Wr, dev)
+        vb, vk, vks = self._coeffs(H, Hr, dev)
+        tmp = torch.empty(B * C * H * cw, dtype=torch.uint8, device=dev)
+        if out is None:
+            out = torch.empty((B, C, ch, cw), dtype=out_dtype, device=dev)
+        ops.clip_image_preprocess(images, Hr, Wr, hb, hk, hks, vb, vk, vks, top, left, ch, cw,
+                                  self.rescale_factor, self.mean, self.std, tmp, out)
+        return out
+
+    def __call__(self, images, out_dtype=torch.float32, device=None):
+        device = device or self.device or torch.device("cuda", torch.cuda.current_device())
+        if isinstance(images, np.ndarray):
+            images = torch.from_numpy(images)
+        if isinstance(images, torch.Tensor):
+            if images.dim() == 3:
+                images = images[None]
+            return self.preprocess_batch(images.to(device), out_dtype)
+        imgs = [torch.as_tensor(im) for im in images]
+        out = torch.empty((len(imgs), imgs[0].shape[0]) + self.crop, dtype=out_dtype, device=device)
+        shapes = {}
+        for i, im in enumerate(imgs):  # one launch per distinct image size
+            shapes.setdefault(tuple(im.shape), []).append(i)
+        for shape, idx in shapes.items():
+            batch = torch.stack([imgs[i] for i in idx]).to(device)
+            res = self.preprocess_batch(batch, out_dtype)
+            out[torch.tensor(idx, device=device)] = res
+        return out
+
+
+@dataclass
+class BatchEncoding:
+    input_ids: torch.Tensor
+    attention_mask: torch.Tensor
+    pixel_values: torch.Tensor | None = None
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+class CuLLaVOProcessor:
+    """LlavaProcessor's __call__ as the reference uses it (text + images, padding=True, 'pt')"""
+
+    def __init__(self, tokenizer, image_processor: ClipImageProcessorHIP | None = None):
+        self.tokenizer = tokenizer
+        self.image_processor = image_processor or ClipImageProcessorHIP()
+
+    def __call__(self, text=None, images=None, padding=True, return_tensors="pt", **kw):
+        texts = [text] if isinstance(text, str) else list(text)
+        seqs = [list(_token_ids(self.tokenizer, t, True).tolist()) for t in texts]
+        n = max(len(s) for s in seqs)
+        pad = self.tokenizer.pad_token_id
+        left = getattr(self.tokenizer, "padding_side", "right") == "left"
+        ids = torch.full((len(seqs), n), pad, dtype=torch.long)
+        mask = torch.zeros((len(seqs), n), dtype=torch.long)
+        for i, s in enumerate(seqs):
+            sl = slice(n - len(s), n) if left else slice(0, len(s))
+            ids[i, sl] = torch.tensor(s, dtype=torch.long)
+            mask[i, sl] = 1
+        pix = self.image_processor(images) if images is not None else None
+        return BatchEncoding(ids, mask, pix)
+
+
+def _outputs(input_ids, pixel_values, attention_mask, labels=None):
+    out = dict.fromkeys(["input_ids", "pixel_values", "attention_mask", "position_ids", "past_key_values",
+                         "inputs_embeds", "vision_feature_layer", "vision_feature_select_strategy", "labels",
+                         "use_cache", "output_attentions", "output_hidden_states", "return_dict"])
+    out.update(input_ids=input_ids, pixel_values=pixel_values, attention_mask=attention_mask, labels=labels)
+    return out
+
+
+def step2_process(batched_inputs, processor, device, ignore_index=-100, image_size=336):
+    """reference cullavo/arch_cullavo.py:397-543 for conversation records: per record the system
+    prompt, then each (question, answer) turn ('<image>' stripped from the first question),
+    images stacked (zeros [3, 336, 336] for text-only records), one processor call, labels
+    right-padded with ignore_index"""
+    images, prompts, labels = [], [], []
+    for batch in batched_inputs:
+        p, lab = make_system_prompt(processor, device, ignore_index)
+        q = batch["question"]
+        for k in range(len(q) // 2):
+            text = q[2 * k]["value"] if k != 0 else q[2 * k]["value"].replace("<image>", "").strip()
+            p, lab = make_and_add_prompt_and_label(p, lab, text, q[2 * k + 1]["value"], processor, device,
+                                                   ignore_index)
+        if "boxes" in batch:
+            raise NotImplementedError("box-drawing prompts need detectron2's Visualizer "
+                                      "(reference cullavo/arch_cullavo.py:438-452): out of scope")
+        if "image" in batch:
+            images.append(torch.as_tensor(batch["image"]))
+        else:
+            images.append(torch.zeros(3, image_size, image_size, dtype=torch.uint8))
+        prompts.append(p)
+        labels.append(lab)
+    enc = processor(text=prompts, images=torch.stack([im.cpu() for im in images]), padding=True,
+                    return_tensors="pt")
+    lab = torch.nn.utils.rnn.pad_sequence([x.cpu() for x in labels], batch_first=True,
+                                          padding_value=ignore_index)
+    return _outputs(enc.input_ids.to(device), enc.pixel_values.to(device) if enc.pixel_values is not None else None,
+                    enc.attention_mask.to(device), lab.to(device))
+
+
+def eval_process(images, aux_prompt=None, prompt=None, processor=None, device=None, ignore_index=-100):
+    """reference cullavo/arch_cullavo.py:63-94"""
+    p, _ = make_system_prompt(processor, device, ignore_index)
+    p += f" {aux_prompt} USER: {prompt} ASSISTANT:" if aux_prompt else f" USER: {prompt} ASSISTANT:"
+    enc = processor(text=p, images=images, padding=True, return_tensors="pt")
+    return {"input_ids": enc.input_ids.to(device), "pixel_values": enc.pixel_values.to(device),
+            "attention_mask": enc.attention_mask.to(device)}
+
+
+def load_lbk_records(json_path: str, image_root: str | None = None):
+    """reference register_lbkllava_datasets.py:25-73 (load_pretrain_arrows + load_pretrain_data):
+    image records are kept only when image_root/<image> exists; boxes are carried through"""
+    with open(json_path) as f:
+        questions = json.load(f)
+    ret = []
+    for q in questions:
+        rec = {"question": q["conversations"], "question_id": q["id"]}
+        if "image" in q:
+            if image_root is None or not os.path.isfile(os.path.join(image_root, q["image"])):
+                continue
+            rec = {"image_id": q["image"], **rec}
+            if "boxes" in q:
+                rec["boxes"] = q["boxes"]
+        ret.append(rec)
+    if not ret:
+        raise AssertionError("No images found in pretraining")
+    return ret

@@ -208,6 +208,27 @@ int cullavo_attn_decode(const void* q, int64_t ldq, const void* k_cache, const v
                         int64_t ld_batch, const int32_t* kv_len, const int32_t* kv_start, void* o, int64_t ldo,
                         int B, int H, int max_len, int D, float scale, float* workspace, void* stream);
 
+/* ---- image preprocessing (data step) --------------------------------
+ * Replaces the CLIPImageProcessor call inside the reference's prompt builders
+ * (cullavo/arch_cullavo.py:82,313,516): PIL-bicubic resize of the shortest edge, center crop,
+ * rescale, normalise -> pixel_values, bit-identical to the CPU processor.
+ * cullavo_resample_coeffs (host only, no GPU): Pillow's precompute_coeffs + 8-bit normalisation
+ * for in_size -> out_size; writes bounds[2*out_size] (first source index, tap count) and
+ * kk[out_size*ksize] (22-bit fixed point); returns ksize (or the ksize alone when bounds or kk
+ * is NULL); bad sizes return CULLAVO_EINVAL (1) like every other entry point.
+ * cullavo_clip_image_preprocess: images uint8 [B, C<=3, H, W] at element strides sb/sc/sy/sx,
+ * resized size Hr x Wr (tables from cullavo_resample_coeffs(W, Wr) and (H, Hr), device copies),
+ * crop window (top, left, crop_h, crop_w); tmp: B*C*H*crop_w bytes; out [B, C, crop_h, crop_w]
+ * f32 or bf16. */
+int cullavo_resample_coeffs(int in_size, int out_size, int32_t* bounds, int32_t* kk, int ksize_cap);
+int cullavo_clip_image_preprocess(const uint8_t* images, int B, int C, int H, int W, int64_t sb, int64_t sc,
+                                  int64_t sy, int64_t sx, int Hr, int Wr, const int32_t* h_bounds,
+                                  const int32_t* h_kk, int h_ksize, const int32_t* v_bounds,
+                                  const int32_t* v_kk, int v_ksize, int top, int left, int crop_h,
+                                  int crop_w, double rescale, float mean0, float mean1, float mean2,
+                                  float std0, float std1, float std2, uint8_t* tmp, void* out,
+                                  int out_dtype, void* stream);
+
 /* ---- embeddings / merge ------------------------------------------------------------------ */
 /* get_input_embeddings()(input_ids) (reference cullavo/arch_cullavo.py:582) */
 int cullavo_embedding_fwd(const int64_t* ids, int64_t n, const void* table, int64_t vocab,

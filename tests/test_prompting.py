@@ -1,0 +1,100 @@
+"""Data step, text half: prompt / label construction and the lbk.json
+records. Fixtures: the REFERENCE's own make_system_prompt / make_and_add_prompt_and_label /
+step2_process over tests/toy_tokenizer.py (tests/golden/make_golden_data.py). CPU only: the
+image processor is replaced by a pass-through here (it has its own tests in test_imageprep.py)."""
+import json
+import os
+import sys
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle import data_oracle as D  # noqa: E402
+from tests.toy_tokenizer import ToyTokenizer  # noqa: E402
+
+GOLD = json.load(open(os.path.join(HERE, "golden", "data_step.json")))
+
+
+class _PassThroughImages:
+    def __call__(self, images):
+        return images.float()
+
+
+def _processor(side="right"):
+    from cullavo_amd.prompting import CuLLaVOProcessor
+    return CuLLaVOProcessor(ToyTokenizer(side), image_processor=_PassThroughImages())
+
+
+def test_system_prompt_and_turn_match_reference():
+    from cullavo_amd import prompting as P
+    g = GOLD["prompts"]["single"]
+    proc = _processor()
+    p, lab = P.make_system_prompt(proc, "cpu", -100)
+    assert p == g["system_prompt"] and len(lab) == g["system_label_len"]
+    p2, lab2 = P.make_and_add_prompt_and_label(p, lab, "What is it?", "A dog.", proc, "cpu", -100)
+    assert p2 == g["prompt"] and lab2.tolist() == g["label"]
+
+
+@pytest.mark.parametrize("side", ["right", "left"])
+def test_step2_process_matches_reference(side):
+    from cullavo_amd import prompting as P
+    g = GOLD["prompts"][side]
+    batch = [dict(r, image=torch.zeros(3, 8, 8, dtype=torch.uint8)) for r in GOLD["records"]]
+    out = P.step2_process(batch, _processor(side), "cpu")
+    assert out["input_ids"].tolist() == g["input_ids"]
+    assert out["attention_mask"].tolist() == g["attention_mask"]
+    assert out["labels"].tolist() == g["labels"]
+    assert out["pixel_values"].shape == (3, 3, 8, 8)
+    assert set(out) >= {"position_ids", "past_key_values", "use_cache", "return_dict"}
+
+
+def test_oracle_restatement_matches_reference_labels():
+    tok = ToyTokenizer()
+    g = GOLD["prompts"]["right"]
+    for rec, labels in zip(GOLD["records"], g["labels"]):
+        _, lab = D.conversation_prompt(rec["question"], tok.encode)
+        assert labels[:len(lab)] == lab and all(x == -100 for x in labels[len(lab):])
+
+
+def test_supervised_tokens_follow_the_answers():
+    """every supervised label is an answer token or '</s>'; the image slots and prompts are -100"""
+    from cullavo_amd import prompting as P
+    tok = ToyTokenizer()
+    rec = GOLD["records"][1]
+    out = P.step2_process([dict(rec, image=torch.zeros(3, 8, 8, dtype=torch.uint8))], _processor(), "cpu")
+    sup = [x for x in out["labels"][0].tolist() if x != -100]
+    answers = []
+    for k in range(len(rec["question"]) // 2):
+        answers += tok.encode(str(rec["question"][2 * k + 1]["value"]) + "</s>", False)
+    assert sup == answers
+    # merged length = text tokens + 575 image slots
+    assert out["labels"].shape[1] == out["input_ids"].shape[1] + 575
+
+
+def test_box_records_raise_and_helpers():
+    from cullavo_amd import prompting as P
+    with pytest.raises(NotImplementedError):
+        P.step2_process([dict(GOLD["records"][0], boxes=[[0, 0, 1, 1]])], _processor(), "cpu")
+    assert P.list2string(["red", "blue", 3]) == "red, blue, 3"
+    assert P.box2string(torch.tensor([0.12345, 0.5, 1.0, 0.0004])) == "[0.123, 0.500, 1.000, 0.000]"
+
+
+def test_load_lbk_records(tmp_path):
+    from cullavo_amd import prompting as P
+    (tmp_path / "img").mkdir()
+    (tmp_path / "img" / "a.jpg").write_bytes(b"x")
+    recs = [{"id": 1, "image": "a.jpg", "conversations": GOLD["records"][0]["question"]},
+            {"id": 2, "image": "missing.jpg", "conversations": []},
+            {"id": 3, "image": "a.jpg", "boxes": [[0, 0, 1, 1]], "conversations": []},
+            {"id": 4, "conversations": GOLD["records"][1]["question"]}]
+    path = tmp_path / "lbk.json"
+    path.write_text(json.dumps(recs))
+    out = P.load_lbk_records(str(path), str(tmp_path / "img"))
+    assert [r["question_id"] for r in out] == [1, 3, 4]
+    assert out[0]["image_id"] == "a.jpg" and "boxes" in out[1] and "image_id" not in out[2]
+    path.write_text(json.dumps(recs[1:2]))
+    with pytest.raises(AssertionError):
+        P.load_lbk_records(str(path), str(tmp_path / "img"))

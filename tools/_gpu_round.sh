@@ -1,6 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 120 --timeout-method thread -k "attn or attention" > gpurun_out/ops_tests.log 2>&1 || exit 1
-timeout -k 10 200 python tools/attn_bench.py > gpurun_out/attn_bench.log 2>&1 || exit 2
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || exit 3
-cat gpurun_out/attn_bench.log; tail -1 gpurun_out/bench.log
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -3 gpurun_out/gpu_tests.log
+timeout -k 10 200 python tools/imageprep_bench.py > gpurun_out/imageprep_bench.log 2>&1 || { cat gpurun_out/imageprep_bench.log; exit 2; }
+cat gpurun_out/imageprep_bench.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 3; }
+tail -2 gpurun_out/smoke.log

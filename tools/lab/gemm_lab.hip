@@ -534,10 +534,6 @@ extern "C" int lab_gemm(int variant, int64_t M, int64_t N, int64_t K, const void
     case 500: return launch_ring<256, 0>(p, s);
     case 501: return launch_ring<256, 1>(p, s);
     case 511: return launch_ring<192, 1>(p, s);
-    case 600: return launch_r2<256, 0>(p, s);
-    case 601: return launch_r2<256, 1>(p, s);
-    case 610: return launch_r2<192, 0>(p, s);
-    case 611: return launch_r2<192, 1>(p, s);
     default: return -1;
   }
 }
