@@ -76,6 +76,27 @@ class CuLLaVOModel(nn.Module):
         return m
 
     # -- reference API -------------------------------------------------------------------------
+    # ---- data step (reference cullavo/arch_cullavo.py:28-94, 397-543) ----
+    @staticmethod
+    def make_system_prompt(processor, device, ignore_index):
+        from .prompting import make_system_prompt
+        return make_system_prompt(processor, device, ignore_index)
+
+    @staticmethod
+    def make_and_add_prompt_and_label(cullavo_prompt, cullavo_label, prompt, answer, processor, device, ignore_index):
+        from .prompting import make_and_add_prompt_and_label
+        return make_and_add_prompt_and_label(cullavo_prompt, cullavo_label, prompt, answer, processor, device,
+                                             ignore_index)
+
+    def step2_process(self, batched_inputs, processor, device):
+        from .prompting import step2_process
+        return step2_process(batched_inputs, processor, device, self.config.ignore_index,
+                             self.config.vision_config.image_size)
+
+    def eval_process(self, images, aux_prompt=None, prompt=None, processor=None, device=None):
+        from .prompting import eval_process
+        return eval_process(images, aux_prompt, prompt, processor, device, self.config.ignore_index)
+
     def get_input_embeddings(self):
         return self.language_model.model.embed_tokens
 

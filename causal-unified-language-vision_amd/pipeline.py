@@ -1,10 +1,12 @@
 """CuLLaVOPipeline and the CuLLaVO model wrapper — drop-ins for reference
 pipeline/CuLLaVOPipeline.py:26-133 and modeling/architectures/cullavo_model.py:12-214.
 
-The reference's forward_step1/2 first turn raw images into prompts on the CPU
-(cullavo/arch_cullavo.py:96-339, detectron2 + tokenizer); that data step is out of scope here
-(SURVEY.md §2, §8(f) row 4), so CuLLaVO.forward accepts the already-tokenised tensors the
-prompt builder would have produced and returns {'loss_llm': loss} like the reference.
+The reference's forward_step1/2 first turn raw records into prompts (cullavo/arch_cullavo.py:96-339,
+397-543). forward_step2 does the same here when it is given lbk.json records and a processor
+(prompting.step2_process: prompt/label builder + GPU image preprocessing); step 1's
+detectron2 box drawing is out of scope, so it (like step 2 without a processor) takes the
+already-tokenised tensors the prompt builder would have produced. Both return
+{'loss_llm': loss} like the reference.
 """
 from __future__ import annotations
 
@@ -50,8 +52,10 @@ class CuLLaVO(nn.Module):
 
     def forward(self, batched_inputs, accel=None, mode=None):
         if self.training:
-            if self.cfg["NAME"] in ("cullavo_step1.yaml", "cullavo_step2.yaml"):
-                return self.forward_step(batched_inputs)
+            if self.cfg["NAME"] == "cullavo_step1.yaml":
+                return self.forward_step1(batched_inputs)
+            if self.cfg["NAME"] == "cullavo_step2.yaml":
+                return self.forward_step2(batched_inputs, accel)
             raise ValueError(f"unknown step config {self.cfg['NAME']}")
         raise NotImplementedError("evaluation / step-2-pre generation needs KV-cache decode (SURVEY.md §8(f) row 2)")
 
@@ -61,7 +65,15 @@ class CuLLaVO(nn.Module):
         return {"loss_llm": out.loss}
 
     forward_step1 = forward_step
-    forward_step2 = forward_step
+
+    def forward_step2(self, batched_inputs, accel=None):
+        """reference cullavo_model.py:78-83: records -> step2_process -> model -> loss"""
+        if isinstance(batched_inputs, (list, tuple)):
+            if self.cullavo_processor is None:
+                raise ValueError("forward_step2 on raw records needs a CuLLaVOProcessor (tokenizer)")
+            device = accel.device if accel is not None else torch.device("cuda", torch.cuda.current_device())
+            batched_inputs = self.cullavo_model.step2_process(batched_inputs, self.cullavo_processor, device)
+        return self.forward_step(batched_inputs)
 
 
 @register_model

@@ -98,3 +98,24 @@ def test_load_lbk_records(tmp_path):
     path.write_text(json.dumps(recs[1:2]))
     with pytest.raises(AssertionError):
         P.load_lbk_records(str(path), str(tmp_path / "img"))
+
+
+@pytest.mark.gpu
+def test_step2_process_on_gpu_with_hip_image_processor():
+    """records with real uint8 images -> step2_process on the GPU: ids / labels as the reference,
+    pixel_values bit-identical to transformers' processor"""
+    import hashlib
+    import numpy as np
+    from cullavo_amd import prompting as P
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden_data import case_image
+    c = next(x for x in json.load(open(os.path.join(HERE, "golden", "data_step.json")))["images"]
+             if x["H"] == 480)
+    img = torch.from_numpy(case_image(c["seed"], c["H"], c["W"]))
+    proc = P.CuLLaVOProcessor(ToyTokenizer(), P.ClipImageProcessorHIP(device="cuda"))
+    batch = [dict(r, image=img) for r in GOLD["records"]]
+    out = P.step2_process(batch, proc, "cuda")
+    g = GOLD["prompts"]["right"]
+    assert out["input_ids"].tolist() == g["input_ids"] and out["labels"].tolist() == g["labels"]
+    for pv in out["pixel_values"]:
+        assert hashlib.sha256(pv.cpu().numpy().astype(np.float32).tobytes()).hexdigest() == c["sha256"]
