@@ -51,6 +51,34 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ d, con
   }
 }
 
+// ---- 16-bit matrix transpose (K-major weight copies for the dX GEMMs) ------------------------
+// 64x64 tiles through LDS: 16-B coalesced loads of source rows, 16-B coalesced stores of
+// destination rows (8 source rows of one column gathered from LDS per thread). HBM-bound:
+// 4 B per element moved.
+__global__ __launch_bounds__(256) void transpose16_k(const u16* __restrict__ src, int64_t lds_, u16* __restrict__ dst,
+                                                     int64_t ldd, int64_t rows, int64_t cols, int64_t tiles_c) {
+  __shared__ u16 tile[64][64 + 8];
+  const int64_t tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int64_t r0 = tr * 64, c0 = tc * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, r = id >> 3, c8 = (id & 7) * 8;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + r < rows && c0 + c8 < cols) v = *(const u16x8*)(src + (r0 + r) * lds_ + c0 + c8);
+    *(u16x8*)&tile[r][c8] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int id = t + k * 256, c = id >> 3, r8 = (id & 7) * 8;
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[r8 + j][c];
+    if (c0 + c < cols && r0 + r8 < rows) *(u16x8*)(dst + (c0 + c) * ldd + r0 + r8) = v;
+  }
+}
+
 // ---- activation backward (projector GELU, CLIP quick_gelu) ---------------------------------
 template <typename T, int ACT>
 __global__ __launch_bounds__(256) void act_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
@@ -361,4 +389,18 @@ extern "C" int cullavo_adamw(void* param, const void* grad, void* exp_avg, void*
   else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype combination");
 #undef ADAM
   return cullavo_check_launch("adamw");
+}
+
+extern "C" int cullavo_transpose16(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, int64_t rows,
+                                   int64_t cols, void* stream) {
+  CV_REQUIRE(rows % 8 == 0 && cols % 8 == 0 && ld_src % 8 == 0 && ld_dst % 8 == 0, CULLAVO_EINVAL,
+             "rows, cols and leading dims must be multiples of 8");
+  CV_REQUIRE(ld_src >= cols && ld_dst >= rows, CULLAVO_EINVAL, "leading dims");
+  CV_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, CULLAVO_EINVAL, "16-B alignment");
+  if (rows == 0 || cols == 0) return CULLAVO_OK;
+  const int64_t tiles_c = cdiv(cols, 64), tiles = cdiv(rows, 64) * tiles_c;
+  CV_REQUIRE(tiles < (1ll << 31), CULLAVO_EINVAL, "matrix too large");
+  transpose16_k<<<(unsigned)tiles, 256, 0, CV_STREAM(stream)>>>((const u16*)src, ld_src, (u16*)dst, ld_dst, rows,
+                                                                cols, tiles_c);
+  return cullavo_check_launch("transpose16");
 }

@@ -122,12 +122,12 @@ class LlamaLayerFn(torch.autograd.Function):
         H, D = cfg.num_attention_heads, cfg.head_dim
         dh3 = dh3.contiguous()
         # MLP
-        da = ops.linear_dx(dh3, layer.mlp.down_proj.weight)
+        da = layer.linear_dx(dh3, "down")
         lg["down"].backward(dh3, a, u_d, da, tr, seed)
         _write_dw(dh3, a, layer.mlp.down_proj.weight)
         dgu = ops.swiglu_bwd(da, gu)
         del da
-        dx2 = ops.linear_dx(dgu, layer.w_gu())
+        dx2 = layer.linear_dx(dgu, "gu")
         lg["gu"].backward(dgu, x2, u_gu, dx2, tr, seed)
         if trainable(layer.mlp.gate_proj.weight):
             g, beta = layer.gu_grad_slot()
@@ -140,7 +140,7 @@ class LlamaLayerFn(torch.autograd.Function):
         commit(wpost)
         del dx2
         # attention
-        do = ops.linear_dx(dh2, layer.self_attn.o_proj.weight)
+        do = layer.linear_dx(dh2, "o")
         lg["o"].backward(dh2, o, u_o, do, tr, seed)
         _write_dw(dh2, o, layer.self_attn.o_proj.weight)
         dqkv = torch.empty_like(qkv)
@@ -150,7 +150,7 @@ class LlamaLayerFn(torch.autograd.Function):
         del do
         ops.rope(dqkv[:, :d], dqkv[:, d:2 * d], sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta,
                  inverse=True)
-        dx1 = ops.linear_dx(dqkv, layer.w_qkv())
+        dx1 = layer.linear_dx(dqkv, "qkv")
         lg["qkv"].backward(dqkv, x1, u_qkv, dx1, tr, seed)
         if trainable(layer.self_attn.q_proj.weight):
             g, beta = layer.qkv_grad_slot()

@@ -9,6 +9,7 @@ fused autograd Functions of functions.py.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -19,6 +20,24 @@ from .arena import ParamArena
 from .config import CLIPVisionConfig, CuLLaVOConfig, LlamaConfig
 from .functions import (ClipLayerFn, EmbeddingFn, LinearFn, LlamaLayerFn, ProjectorFn, StepContext)
 from .lora import NO_LORA, LoraGroup, LoraSettings, lm_groups, lora_specs, vision_groups
+
+# dX GEMMs of the decoder layers can read K-major weight copies: "side" refreshes them on a side
+# HIP stream during the forward, "sync" on the compute stream at first use, "off" (default) reads
+# W [N, K] along N (gemm mode (0,1)). All three give bitwise-equal gradients. Measured on the
+# MI355X (config 3): isolated dX GEMMs gain 5-18 %, but in the step the gain (~5 ms) is eaten by
+# the per-step re-transposes (~4.5 ms at 5-6 TB/s) in full fine-tune, and the LoRA recipe
+# (frozen copies, made once) moved by +0.1 % -- so the 13 GB of copies are not kept by default.
+KMAJOR_MODE = os.environ.get("CULLAVO_KMAJOR", "off")
+if KMAJOR_MODE not in ("side", "sync", "off"):
+    raise ValueError(f"CULLAVO_KMAJOR={KMAJOR_MODE!r}: expected side | sync | off")
+_SIDE: dict = {}
+
+
+def _side_stream(device):
+    key = torch.device(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=key)
+    return _SIDE[key]
 
 
 class _Box(nn.Module):
@@ -356,6 +375,28 @@ class LlamaDecoderLayer(nn.Module):
         self._arena.mark_written([self._lp + f"self_attn.{n}_proj.weight" for n in "kv"])
         return g, beta
 
+    def _kmajor_specs(self):
+        d, F = self.cfg.hidden_size, self.cfg.intermediate_size
+        lp = self._lp
+        return {"qkv": (lp + "self_attn.q_proj.weight", (3 * d, d)), "o": (lp + "self_attn.o_proj.weight", (d, d)),
+                "gu": (lp + "mlp.gate_proj.weight", (2 * F, d)), "down": (lp + "mlp.down_proj.weight", (d, F))}
+
+    def prefetch_kmajor(self):
+        """Refresh this layer's K-major weight copies on the side stream while its forward runs
+        (KMAJOR_MODE "side"), so the backward's dX GEMMs read reduction-contiguous weights."""
+        if KMAJOR_MODE == "off":
+            return
+        st = _side_stream(self._arena.device) if KMAJOR_MODE == "side" else None
+        for key, shape in self._kmajor_specs().values():
+            self._arena.prefetch_transposed(key, shape, st)
+
+    def linear_dx(self, dy, which: str):
+        """dx = dy @ W for which in qkv | o | gu | down (fused weights), via the K-major copy."""
+        key, shape = self._kmajor_specs()[which]
+        if KMAJOR_MODE == "off":
+            return ops.linear_dx(dy, self._arena.view(key, shape))
+        return ops.linear_dx_t(dy, self._arena.transposed(key, shape))
+
     def gu_grad_slot(self):
         g, beta = self._arena.grad_slot(self._lp + "mlp.gate_proj.weight",
                                         (2 * self.cfg.intermediate_size, self.cfg.hidden_size))
@@ -366,6 +407,8 @@ class LlamaDecoderLayer(nn.Module):
         return [p for p in self.parameters() if p.requires_grad]
 
     def run(self, h2d, sctx: StepContext):
+        if torch.is_grad_enabled() and h2d.requires_grad:
+            self.prefetch_kmajor()
         return LlamaLayerFn.apply(h2d, self, sctx, *self.fn_params())
 
 

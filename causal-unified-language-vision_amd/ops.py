@@ -14,7 +14,7 @@ import torch
 from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, DT_BF16, DT_F32, call, lib
 
 __all__ = [
-    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "gemm_ex", "linear", "linear_dx", "linear_dw",
+    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "gemm_ex", "linear", "linear_dx", "linear_dx_t", "transpose2d", "linear_dw",
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "swiglu_fwd", "swiglu_bwd",
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
@@ -168,6 +168,31 @@ def linear_dx(dy, w, *, residual=None, out=None):
     gemm(0, 1, M, K, N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), residual=residual,
          ldr=_ld(residual) if residual is not None else 0)
     return dx
+
+
+def linear_dx_t(dy, wt, *, residual=None, out=None):
+    """dx = dy @ wt.T (+ residual); dy [M,N], wt [K,N] (the K-major copy of w [N,K], ParamArena
+    .transposed): both operands reduction-contiguous, bitwise equal to linear_dx(dy, w)."""
+    M, N = dy.shape
+    K = wt.shape[0]
+    if wt.shape[1] != N:
+        raise ValueError(f"linear_dx_t: dy {tuple(dy.shape)} vs wt {tuple(wt.shape)}")
+    dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
+    gemm(0, 0, M, K, N, dy, _ld(dy), wt, _ld(wt), dx, _ld(dx), residual=residual,
+         ldr=_ld(residual) if residual is not None else 0)
+    return dx
+
+
+def transpose2d(src, dst):
+    """dst[c, r] = src[r, c] for 16-bit matrices (cullavo_transpose16); returns dst."""
+    _dev(src, dst)
+    if src.dtype not in (torch.bfloat16, torch.float16) or dst.dtype != src.dtype:
+        raise ValueError("transpose2d: bf16/fp16 tensors of one dtype")
+    rows, cols = src.shape
+    if dst.shape != (cols, rows) or src.stride(1) != 1 or dst.stride(1) != 1:
+        raise ValueError(f"transpose2d: src {tuple(src.shape)} -> dst {tuple(dst.shape)} (row-major)")
+    call("transpose16", _ptr(src), src.stride(0), _ptr(dst), dst.stride(0), rows, cols, _stream())
+    return dst
 
 
 def linear_dw(dy, x, out, *, beta: float = 0.0):

@@ -55,6 +55,7 @@ class FusedAdamW(torch.optim.Optimizer):
         for a, (m, v) in zip(self.arenas, self.flat_state):
             ops.adamw(a.flat, a.grad_flat, m, v, lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"],
                       weight_decay=g["weight_decay"], step=self.step_count, grad_scale=scale)
+            a.note_written()
         self._clip_pending = False
 
     def zero_grad(self, set_to_none: bool = False):

@@ -139,6 +139,7 @@ class DefaultTrainer:
         """identical replicas at start (one RCCL broadcast per arena from rank 0)"""
         for ar in cm.arenas.values():
             dist.broadcast(ar.flat, src=0)
+            ar.note_written()
 
     def train(self):
         self.init_train()

@@ -154,6 +154,12 @@ int cullavo_swiglu_fwd(const void* gu, int64_t rows, int64_t F, void* out, int d
                        void* stream);
 int cullavo_swiglu_bwd(const void* dout, const void* gu, int64_t rows, int64_t F, void* dgu,
                        int dtype, void* stream);
+/* dst[c, r] = src[r, c] for a 16-bit matrix (bf16/fp16) [rows, cols], leading dims in elements.
+ * Keeps a K-major copy of a Linear weight W [N, K] so that the input gradient dx = dy @ W
+ * (reference: autograd of F.linear, tf:llama/modeling_llama.py:163-176 / :281-300) runs with
+ * both GEMM operands reduction-contiguous. rows, cols, ld_src, ld_dst must be multiples of 8. */
+int cullavo_transpose16(const void* src, int64_t ld_src, void* dst, int64_t ld_dst, int64_t rows,
+                        int64_t cols, void* stream);
 /* dx = dy * act'(preact) for CULLAVO_ACT_GELU / CULLAVO_ACT_QUICK_GELU */
 int cullavo_act_bwd(int act, const void* dy, const void* preact, void* dx, int64_t n, int dtype,
                     void* stream);

@@ -129,3 +129,32 @@ def test_full_size_layer_shapes_run():
     gflat = m.arenas["layers"].grad_flat
     assert torch.isfinite(gflat.float()).all()
     assert gflat.float().abs().sum() > 0
+
+
+def test_kmajor_weight_copies_bitwise_and_refreshed(monkeypatch):
+    """The decoder layers' dX GEMMs from K-major weight copies (side-stream or synchronous
+    refresh) give gradients bitwise equal to the N-major path over two AdamW steps (the copies are
+    re-made after each step) and after an in-place torch write to a layer weight."""
+    import cullavo_amd.modeling as MD
+    from cullavo_amd.optim import FusedAdamW
+    ids, mask, pix, labels = inputs()
+    grads = {}
+    for mode in ("off", "sync", "side"):
+        monkeypatch.setattr(MD, "KMAJOR_MODE", mode)
+        m = build()
+        opt = FusedAdamW(list(m.arenas.values()), lr=1e-3)
+        seen = []
+        for step in range(3):
+            if step == 2:
+                with torch.no_grad():
+                    m.arenas["layers"].params["language_model.model.layers.0.mlp.down_proj.weight"].mul_(0.5)
+            opt.zero_grad()
+            out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
+            out.loss.backward()
+            torch.cuda.synchronize()
+            seen.append(m.arenas["layers"].grad_flat.clone())
+            opt.step()
+        grads[mode] = seen
+    for mode in ("sync", "side"):
+        for s, (a, b) in enumerate(zip(grads["off"], grads[mode])):
+            assert torch.equal(a, b), f"mode {mode} step {s}"

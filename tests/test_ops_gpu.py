@@ -464,3 +464,34 @@ def test_linear_dw_ragged_token_count():
     dw = torch.empty((N, K), dtype=torch.float32, device=DEV)
     ops().linear_dw(dy.to(DEV), x.to(DEV), dw)
     close(dw, dy.float().T @ x.float(), 1e-5, "dw ragged")
+
+
+@pytest.mark.parametrize("rows,cols,pad", [(64, 64, 0), (72, 136, 0), (4096, 11008, 0), (200, 96, 24)])
+def test_transpose16_exact(rows, cols, pad):
+    """cullavo_transpose16 (K-major weight copies for the dX GEMMs) == torch .t(), ragged tiles and
+    padded leading dims included"""
+    from cullavo_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(rows + cols)
+    base = torch.randn(rows, cols + pad, device="cuda", generator=g).bfloat16()
+    src = base[:, :cols]
+    dst = torch.full((cols, rows), 7.0, device="cuda", dtype=torch.bfloat16)
+    ops.transpose2d(src, dst)
+    assert torch.equal(dst, src.t())
+    with pytest.raises(Exception):
+        ops.transpose2d(src[:, :cols - 4], torch.empty(cols - 4, rows, device="cuda", dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(8704, 4096, 4096), (300, 1024, 640), (8704, 11008, 4096)])
+def test_linear_dx_kmajor_bitwise(M, N, K):
+    """dx from the K-major copy (gemm mode (0,0)) is bitwise equal to dx = dy @ W read along N
+    (mode (0,1)): same K-tile order, same MFMA sequence"""
+    from cullavo_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    w = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    wt = ops.transpose2d(w, torch.empty(K, N, device="cuda", dtype=torch.bfloat16))
+    a = ops.linear_dx(dy, w)
+    b = ops.linear_dx_t(dy, wt)
+    assert torch.equal(a, b)
+    ref = dy.float() @ w.float()
+    assert ((b.float() - ref).norm() / ref.norm()).item() < 1e-2
