@@ -245,24 +245,45 @@ __global__ __launch_bounds__(256) void scale_k(T* __restrict__ x, int64_t n, con
 
 // torch.optim.AdamW (single-tensor math): p *= 1-lr*wd; m = lerp(m, g, 1-b1);
 // v = b2*v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+// (one element, with the stored dtypes' roundings)
+template <typename T, typename S>
+DEV void adamw_elem(float gv, float& pv, float& mv, float& vv, float lr, float b1, float b2, float eps, float wd,
+                    float bc2_sqrt, float step_size) {
+#pragma clang fp contract(off)  // no FMA fusion: the 8-wide and element-wise paths round alike
+  pv = Elt<T>::rnd(pv * (1.f - lr * wd));
+  mv = Elt<S>::rnd(mv + (gv - mv) * (1.f - b1));
+  vv = Elt<S>::rnd(vv * b2 + (1.f - b2) * gv * gv);
+  const float denom = sqrtf(vv) / bc2_sqrt + eps;
+  pv = pv - step_size * mv / denom;
+}
+
+// 8 elements per lane per access (16 B of bf16 params / grads, 16 or 32 B of state), so the
+// 14-22 B/param stream is issued as full-width loads; the scalar loop takes the tail (and every
+// element when a buffer is not 16-B aligned: vec = false).
 template <typename T, typename S>
 __global__ __launch_bounds__(256) void adamw_k(T* __restrict__ p, const T* __restrict__ g,
                                                S* __restrict__ m, S* __restrict__ v, int64_t n,
                                                float lr, float b1, float b2, float eps, float wd,
                                                float bc1, float bc2_sqrt,
-                                               const float* __restrict__ gscale) {
+                                               const float* __restrict__ gscale, bool vec) {
   const float gs = gscale ? gscale[0] : 1.f;
   const float step_size = lr / bc1;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gv = Elt<T>::ld(g, i) * gs;
-    float pv = Elt<T>::ld(p, i);
-    float mv = Elt<S>::ld(m, i);
-    float vv = Elt<S>::ld(v, i);
-    pv = Elt<T>::rnd(pv * (1.f - lr * wd));
-    mv = Elt<S>::rnd(mv + (gv - mv) * (1.f - b1));
-    vv = Elt<S>::rnd(vv * b2 + (1.f - b2) * gv * gv);
-    const float denom = sqrtf(vv) / bc2_sqrt + eps;
-    pv = pv - step_size * mv / denom;
+  const int64_t nvec = vec ? n / 8 : 0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float gv[8], pv[8], mv[8], vv[8];
+    load8(g + i * 8, gv);
+    load8(p + i * 8, pv);
+    load8(m + i * 8, mv);
+    load8(v + i * 8, vv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adamw_elem<T, S>(gv[j] * gs, pv[j], mv[j], vv[j], lr, b1, b2, eps, wd, bc2_sqrt, step_size);
+    store8(p + i * 8, pv);
+    store8(m + i * 8, mv);
+    store8(v + i * 8, vv);
+  }
+  for (int64_t i = nvec * 8 + blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float pv = Elt<T>::ld(p, i), mv = Elt<S>::ld(m, i), vv = Elt<S>::ld(v, i);
+    adamw_elem<T, S>(Elt<T>::ld(g, i) * gs, pv, mv, vv, lr, b1, b2, eps, wd, bc2_sqrt, step_size);
     Elt<T>::st(p, i, pv);
     Elt<S>::st(m, i, mv);
     Elt<S>::st(v, i, vv);
@@ -381,8 +402,9 @@ extern "C" int cullavo_adamw(void* param, const void* grad, void* exp_avg, void*
   hipStream_t s = CV_STREAM(stream);
   const float bc1 = 1.f - (float)std::pow((double)beta1, (double)step);
   const float bc2s = (float)std::sqrt(1.0 - std::pow((double)beta2, (double)step));
-  const int g = ew_grid(n);
-#define ADAM(T, S) adamw_k<T, S><<<g, 256, 0, s>>>((T*)param, (const T*)grad, (S*)exp_avg, (S*)exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale)
+  const bool vec = (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0;
+  const int g = ew_grid(vec ? n / 8 : n);
+#define ADAM(T, S) adamw_k<T, S><<<g, 256, 0, s>>>((T*)param, (const T*)grad, (S*)exp_avg, (S*)exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, grad_scale, vec)
   if (dtype == CULLAVO_DT_BF16 && state_dtype == CULLAVO_DT_BF16) ADAM(u16, u16);
   else if (dtype == CULLAVO_DT_BF16 && state_dtype == CULLAVO_DT_F32) ADAM(u16, float);
   else if (dtype == CULLAVO_DT_F32 && state_dtype == CULLAVO_DT_F32) ADAM(float, float);

@@ -495,3 +495,30 @@ def test_linear_dx_kmajor_bitwise(M, N, K):
     assert torch.equal(a, b)
     ref = dy.float() @ w.float()
     assert ((b.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("state_dtype", [torch.bfloat16, torch.float32])
+def test_adamw_vector_path_bitwise_equals_scalar_path(state_dtype):
+    """The 8-wide AdamW path (16-B aligned buffers) and the element-wise path (a buffer offset
+    by one element) give bitwise-equal params and moments; n is ragged so the tail runs too."""
+    n = 3 * 65536 + 13
+    g0 = torch.Generator(device="cuda").manual_seed(5)
+    base = {k: torch.randn(n + 8, device="cuda", generator=g0) * 0.1 for k in ("p", "g")}
+    outs = []
+    for off in (0, 1):
+        p = base["p"].bfloat16()[:n].clone() if off == 0 else _misaligned(base["p"].bfloat16(), n)
+        g = base["g"].bfloat16()[:n].clone() if off == 0 else _misaligned(base["g"].bfloat16(), n)
+        m = torch.zeros(n + 8, device="cuda", dtype=state_dtype)[off:off + n]
+        v = torch.zeros(n + 8, device="cuda", dtype=state_dtype)[off:off + n]
+        for step in (1, 2, 3):
+            ops().adamw(p, g, m, v, lr=1e-2, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.1, step=step)
+        outs.append((p.clone(), m.clone(), v.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def _misaligned(t, n):
+    buf = torch.empty(n + 8, device=t.device, dtype=t.dtype)
+    view = buf[1:1 + n]
+    view.copy_(t[:n])
+    return view
