@@ -206,6 +206,50 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ q, int64_t ldq, T*
   if (k != nullptr) rope_heads<T>(k + t * ldk, ldk, hk, half, i4, hslot, nslot, c, s, inverse);
 }
 
+// 16-B variant: the block computes the token's half-D (cos, sin) pairs once into LDS (same f32
+// formula and rounding as rope_k, which evaluated them 16x redundantly per thread), then each
+// item = (head, group of 8 frequencies) moves x1[8] and x2[8] with one 16-B load/store each.
+// Needs D % 16 == 0 and 16-B aligned rows.
+template <typename T>
+__global__ __launch_bounds__(256) void rope8_k(T* __restrict__ q, int64_t ldq, T* __restrict__ k,
+                                               int64_t ldk, const int64_t* __restrict__ pos, int hq,
+                                               int hk, int D, float theta, int inverse) {
+  __shared__ float cs[256], sn[256];
+  const int64_t t = blockIdx.x;
+  const int half = D / 2, ng = half / 8;
+  if (threadIdx.x < half) {
+    const int i = threadIdx.x;
+    const float inv_freq = 1.0f / powf(theta, (float)(2 * i) / (float)D);
+    const float ang = (float)pos[t] * inv_freq;
+    cs[i] = Elt<T>::rnd(cosf(ang));
+    sn[i] = Elt<T>::rnd(sinf(ang));
+  }
+  __syncthreads();
+  const int nq = hq * ng, nall = (hq + (k != nullptr ? hk : 0)) * ng;
+  for (int it = threadIdx.x; it < nall; it += 256) {
+    const bool isq = it < nq;
+    const int w = isq ? it : it - nq, h = w / ng, g8 = (w % ng) * 8;
+    T* p1 = (isq ? q + t * ldq : k + t * ldk) + (int64_t)h * D + g8;
+    T* p2 = p1 + half;
+    float x1[8], x2[8], o1[8], o2[8];
+    load8(p1, x1);
+    load8(p2, x2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = cs[g8 + j], sv = sn[g8 + j];
+      if (!inverse) {
+        o1[j] = Elt<T>::rnd(Elt<T>::rnd(x1[j] * c) + Elt<T>::rnd(-x2[j] * sv));
+        o2[j] = Elt<T>::rnd(Elt<T>::rnd(x2[j] * c) + Elt<T>::rnd(x1[j] * sv));
+      } else {
+        o1[j] = x1[j] * c + x2[j] * sv;
+        o2[j] = x2[j] * c - x1[j] * sv;
+      }
+    }
+    store8(p1, o1);
+    store8(p2, o2);
+  }
+}
+
 // ---- optimiser ------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
@@ -362,6 +406,15 @@ extern "C" int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const in
   CV_REQUIRE(head_dim % 8 == 0 && head_dim >= 8 && head_dim / 8 <= 256, CULLAVO_EINVAL, "head_dim");
   if (tokens == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
+  const uintptr_t al = (uintptr_t)q | (uintptr_t)k;
+  const bool vec = head_dim % 16 == 0 && head_dim <= 512 && ldq % 8 == 0 && (k == nullptr || ldk % 8 == 0) &&
+                   (al & 15) == 0;
+  if (vec) {
+    if (dtype == CULLAVO_DT_BF16) rope8_k<u16><<<(unsigned)tokens, 256, 0, s>>>((u16*)q, ldq, (u16*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
+    else if (dtype == CULLAVO_DT_F32) rope8_k<float><<<(unsigned)tokens, 256, 0, s>>>((float*)q, ldq, (float*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
+    else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+    return cullavo_check_launch("rope");
+  }
   if (dtype == CULLAVO_DT_BF16) rope_k<u16><<<(unsigned)tokens, 256, 0, s>>>((u16*)q, ldq, (u16*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
   else if (dtype == CULLAVO_DT_F32) rope_k<float><<<(unsigned)tokens, 256, 0, s>>>((float*)q, ldq, (float*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
   else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");

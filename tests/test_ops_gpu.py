@@ -522,3 +522,20 @@ def _misaligned(t, n):
     view = buf[1:1 + n]
     view.copy_(t[:n])
     return view
+
+
+@pytest.mark.parametrize("D,H,inverse", [(128, 32, 0), (128, 32, 1), (64, 3, 0), (16, 5, 1)])
+def test_rope_vector_path_bitwise_equals_element_path(D, H, inverse):
+    """rope8_k (LDS cos/sin table, 16-B rows) and rope_k (4-wide, taken for rows that are not
+    16-B aligned) give bitwise-equal q and k, forward and inverse, on the fused q|k|v layout."""
+    T = 70
+    g = torch.Generator(device="cuda").manual_seed(D + H)
+    qkv = torch.randn(T, 3 * H * D, device="cuda", generator=g).bfloat16()
+    pos = torch.randint(0, 1100, (T,), device="cuda", generator=g)
+    a = qkv.clone()
+    ops().rope(a[:, :H * D], a[:, H * D:2 * H * D], pos, hq=H, hk=H, head_dim=D, theta=10000.0, inverse=inverse)
+    buf = torch.empty(T * 3 * H * D + 1, device="cuda", dtype=torch.bfloat16)
+    b = buf[1:].view(T, 3 * H * D)  # 2-B offset: not 16-B aligned -> element path
+    b.copy_(qkv)
+    ops().rope(b[:, :H * D], b[:, H * D:2 * H * D], pos, hq=H, hk=H, head_dim=D, theta=10000.0, inverse=inverse)
+    assert torch.equal(a, b)
