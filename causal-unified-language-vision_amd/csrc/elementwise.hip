@@ -251,8 +251,11 @@ __global__ __launch_bounds__(256) void rope8_k(T* __restrict__ q, int64_t ldq, T
 }
 
 // ---- optimiser ------------------------------------------------------------------------------
+// block b sums a fixed grid-stride subset in a fixed order (lane accumulation, then the wave
+// tree, then waves 0..3) into partials[b]; sumsq_final_k adds the partials to out[0] in a
+// fixed tree order. Same inputs -> same bits, whatever the scheduling.
 template <typename T>
-__global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t n, float* __restrict__ partials) {
   __shared__ float red[4];
   float acc = 0.f;
   const int64_t nvec = n / 8;
@@ -271,7 +274,18 @@ __global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t 
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_k(const float* __restrict__ partials, int np,
+                                                     float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < np; i += 256) acc += partials[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] += (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ void clip_coef_k(const float* sumsq, float max_norm, float* coef, float* norm_out) {
@@ -421,13 +435,17 @@ extern "C" int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const in
   return cullavo_check_launch("rope");
 }
 
-extern "C" int cullavo_sumsq(const void* x, int64_t n, float* out, int dtype, void* stream) {
+extern "C" int cullavo_sumsq(const void* x, int64_t n, float* out, float* partials, int dtype, void* stream) {
   if (n == 0) return CULLAVO_OK;
+  CV_REQUIRE(partials != nullptr, CULLAVO_EINVAL, "partials workspace (CULLAVO_SUMSQ_PARTIALS floats)");
+  CV_REQUIRE(dtype != CULLAVO_DT_BF16 || ((uintptr_t)x & 15) == 0, CULLAVO_EINVAL, "x must be 16-B aligned");
+  CV_REQUIRE(dtype != CULLAVO_DT_F32 || ((uintptr_t)x & 15) == 0, CULLAVO_EINVAL, "x must be 16-B aligned");
   hipStream_t s = CV_STREAM(stream);
-  const int g = ew_grid(n / 8 + 1);
-  if (dtype == CULLAVO_DT_BF16) sumsq_k<u16><<<g, 256, 0, s>>>((const u16*)x, n, out);
-  else if (dtype == CULLAVO_DT_F32) sumsq_k<float><<<g, 256, 0, s>>>((const float*)x, n, out);
+  const int g = (int)std::min<int64_t>(CULLAVO_SUMSQ_PARTIALS, std::max<int64_t>(1, cdiv(n / 8, 256)));
+  if (dtype == CULLAVO_DT_BF16) sumsq_k<u16><<<g, 256, 0, s>>>((const u16*)x, n, partials);
+  else if (dtype == CULLAVO_DT_F32) sumsq_k<float><<<g, 256, 0, s>>>((const float*)x, n, partials);
   else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
+  sumsq_final_k<<<1, 256, 0, s>>>(partials, g, out);
   return cullavo_check_launch("sumsq");
 }
 

@@ -443,9 +443,20 @@ def adamw(param, grad, exp_avg, exp_avg_sq, *, lr: float, beta1: float, beta2: f
          _dt(exp_avg), _stream())
 
 
+SUMSQ_PARTIALS = 1024  # CULLAVO_SUMSQ_PARTIALS
+_SUMSQ_WS: dict = {}
+
+
 def sumsq(x, out):
+    """out[0] += sum(x^2), deterministic (fixed-order block partials in a cached f32 workspace;
+    calls are stream-ordered, so one workspace per device serves them all)"""
     _dev(x, out)
-    call("sumsq", _ptr(x), x.numel(), _ptr(out), _dt(x), _stream())
+    if not x.is_contiguous():
+        raise ValueError("sumsq: x must be contiguous")
+    ws = _SUMSQ_WS.get(x.device)
+    if ws is None:
+        ws = _SUMSQ_WS[x.device] = torch.empty(SUMSQ_PARTIALS, dtype=torch.float32, device=x.device)
+    call("sumsq", _ptr(x), x.numel(), _ptr(out), _ptr(ws), _dt(x), _stream())
 
 
 def clip_coef(sumsq_buf, max_norm: float, coef, norm_out=None):

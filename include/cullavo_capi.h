@@ -291,8 +291,13 @@ int cullavo_ce_bwd(const void* logits, int64_t ldl, const int64_t* targets, cons
 int cullavo_adamw(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
                   float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
                   const float* grad_scale, int dtype, int state_dtype, void* stream);
-/* out[0] += sum(grad^2) (f32, device); run over every grad buffer, then cullavo_clip_coef */
-int cullavo_sumsq(const void* x, int64_t n, float* out, int dtype, void* stream);
+/* out[0] += sum(grad^2) (f32, device); run over every grad buffer, then cullavo_clip_coef.
+ * Deterministic: CULLAVO_SUMSQ_PARTIALS block sums land in the caller's f32 workspace
+ * `partials` and one block adds them to out[0] in a fixed order (no float atomics), so the
+ * global norm and the clip coefficient are identical run to run, like torch's
+ * clip_grad_norm_ (reference pipeline/CuLLaVOPipeline.py:90). */
+#define CULLAVO_SUMSQ_PARTIALS 1024
+int cullavo_sumsq(const void* x, int64_t n, float* out, float* partials, int dtype, void* stream);
 /* coef[0] = min(1, max_norm / (sqrt(sumsq[0]) + 1e-6)); norm_out[0] = sqrt(sumsq[0]) */
 int cullavo_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out,
                       void* stream);

@@ -539,3 +539,17 @@ def test_rope_vector_path_bitwise_equals_element_path(D, H, inverse):
     b.copy_(qkv)
     ops().rope(b[:, :H * D], b[:, H * D:2 * H * D], pos, hq=H, hk=H, head_dim=D, theta=10000.0, inverse=inverse)
     assert torch.equal(a, b)
+
+
+def test_sumsq_deterministic_and_accurate():
+    """the grad-norm sum of squares is bit-identical across repeats (fixed-order partials, no
+    float atomics) and matches a float64 sum; ragged n exercises the tail"""
+    x = (torch.randn(50_000_003, device=DEV) * 1e-2).bfloat16()
+    vals = []
+    for _ in range(5):
+        acc = torch.zeros(1, device=DEV)
+        ops().sumsq(x, acc)
+        vals.append(acc.item())
+    assert len(set(vals)) == 1
+    ref = x.double().pow(2).sum().item()
+    assert abs(vals[0] - ref) <= 1e-5 * ref
