@@ -167,66 +167,106 @@ __global__ __launch_bounds__(256) void vision_embed_ln_k(const u16* __restrict__
 }
 
 // ---- llava merge plan (transformers ~4.37 _merge_input_ids_with_image_features) ------------
-// One thread per batch row for the per-row scans (B <= 1024), then a serial prefix over rows
-// for the flattened image-row numbering (image features fill the slots in (b, l) order).
-__global__ void merge_plan_k(const int64_t* __restrict__ ids, const int64_t* __restrict__ mask, int B,
-                             int S, int L, int64_t image_token, int64_t P, int left_padding,
-                             int64_t* __restrict__ text_dst, int64_t* __restrict__ src,
-                             int64_t* __restrict__ mmask, int64_t* __restrict__ pos) {
-  __shared__ int64_t img_slots[1024];
-  const int b = threadIdx.x;
-  if (b < B) {
+// One 1024-thread workgroup walks the batch rows in order (the image rows are numbered across
+// the flattened (b, l) order, carried in `base`); inside a row every step is a workgroup-wide
+// scan over 1024-element chunks, so the row costs a few scans instead of the L-long serial
+// loops of one thread per row (806 -> tens of us at B=8, L=1088).
+constexpr int kMergeThreads = 1024;
+
+// inclusive scan over the workgroup; *total = sum over all threads
+DEV int64_t wg_incl_scan(int64_t v, int64_t* lds, int64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) lds[w] = v;
+  __syncthreads();
+  int64_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kMergeThreads / 64; ++k) {
+    const int64_t x = lds[k];
+    off += k < w ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return v + off;
+}
+
+__global__ __launch_bounds__(kMergeThreads) void merge_plan_k(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ mask, int B, int S, int L, int64_t image_token,
+    int64_t P, int left_padding, int64_t* __restrict__ text_dst, int64_t* __restrict__ src,
+    int64_t* __restrict__ mmask, int64_t* __restrict__ pos) {
+  __shared__ int64_t lds[kMergeThreads / 64];
+  const int t = threadIdx.x;
+  const int64_t n_text = (int64_t)B * S;
+  int64_t base = 0;  // image rows numbered so far (flattened (b, l) order)
+  for (int b = 0; b < B; ++b) {
     const int64_t* idr = ids + (int64_t)b * S;
     const int64_t* mr = mask ? mask + (int64_t)b * S : nullptr;
     int64_t* srow = src + (int64_t)b * L;
     int64_t* mmrow = mmask + (int64_t)b * L;
-    for (int l = 0; l < L; ++l) { srow[l] = -2; mmrow[l] = 0; }  // -2: not a text slot yet
-    // new_token_positions = cumsum(is_img * (P - 1) + 1) - 1
-    int64_t last = -1;
-    for (int s = 0; s < S; ++s) last += (idr[s] == image_token) ? P : 1;
-    const int64_t nb_pad = (int64_t)L - 1 - last;
-    int64_t np = -1;
-    for (int s = 0; s < S; ++s) {
-      const bool img = idr[s] == image_token;
-      np += img ? P : 1;
-      const int64_t dst = np + (left_padding ? nb_pad : 0);
-      if (img) {
-        text_dst[(int64_t)b * S + s] = -1;
-      } else {
-        text_dst[(int64_t)b * S + s] = dst;
-        if (dst >= 0 && dst < L) {
-          srow[dst] = (int64_t)b * S + s;
-          mmrow[dst] = mr ? mr[s] : 1;
+    int64_t* prow = pos + (int64_t)b * L;
+    // new_token_positions = cumsum(is_img * (P - 1) + 1) - 1; last = its final value
+    int64_t total = 0, tot;
+    for (int c0 = 0; c0 < S; c0 += kMergeThreads) {
+      const int s = c0 + t;
+      wg_incl_scan(s < S ? (idr[s] == image_token ? P : 1) : 0, lds, &tot);
+      total += tot;
+    }
+    const int64_t nb_pad = (int64_t)L - 1 - (total - 1);
+    for (int l = t; l < L; l += kMergeThreads) { srow[l] = -2; mmrow[l] = 0; }  // -2: not a text slot yet
+    __syncthreads();
+    int64_t carry = -1;
+    for (int c0 = 0; c0 < S; c0 += kMergeThreads) {
+      const int s = c0 + t;
+      const bool img = s < S && idr[s] == image_token;
+      const int64_t np = carry + wg_incl_scan(s < S ? (img ? P : 1) : 0, lds, &tot);
+      carry += tot;
+      if (s < S) {
+        const int64_t dst = np + (left_padding ? nb_pad : 0);
+        if (img) {
+          text_dst[(int64_t)b * S + s] = -1;
+        } else {
+          text_dst[(int64_t)b * S + s] = dst;
+          if (dst >= 0 && dst < L) {
+            srow[dst] = (int64_t)b * S + s;
+            mmrow[dst] = mr ? mr[s] : 1;
+          }
         }
       }
     }
-    // image_to_overwrite = not-a-text-slot & (cumsum - 1 >= nb_pad); count them
-    int64_t cnt = 0, cs = 0;
-    for (int l = 0; l < L; ++l) {
-      if (srow[l] == -2) {
-        cs += 1;
-        if (cs - 1 >= nb_pad) { srow[l] = -3; cnt += 1; }  // -3: image slot (numbered below)
+    __syncthreads();
+    // image_to_overwrite = not-a-text-slot & (cumsum - 1 >= nb_pad); image slots get the next
+    // image rows in order and mask |= 1; the other free slots stay -1
+    int64_t cs_carry = 0, rank_carry = 0;
+    for (int c0 = 0; c0 < L; c0 += kMergeThreads) {
+      const int l = c0 + t;
+      const bool fr = l < L && srow[l] == -2;
+      const int64_t cs = cs_carry + wg_incl_scan(fr ? 1 : 0, lds, &tot);
+      cs_carry += tot;
+      const bool slot = fr && cs - 1 >= nb_pad;
+      const int64_t rk = rank_carry + wg_incl_scan(slot ? 1 : 0, lds, &tot) - (slot ? 1 : 0);
+      rank_carry += tot;
+      if (fr) {
+        if (slot) { srow[l] = n_text + base + rk; mmrow[l] = 1; }
         else srow[l] = -1;
       }
     }
-    img_slots[b] = cnt;
-  }
-  __syncthreads();
-  if (b < B) {
-    int64_t base = 0;
-    for (int k = 0; k < b; ++k) base += img_slots[k];
-    int64_t* srow = src + (int64_t)b * L;
-    int64_t* mmrow = mmask + (int64_t)b * L;
-    const int64_t n_text = (int64_t)B * S;
-    for (int l = 0; l < L; ++l) {
-      if (srow[l] == -3) { srow[l] = n_text + base++; mmrow[l] = 1; }  // mask |= image slot
-    }
+    base += rank_carry;
+    __syncthreads();
     // position_ids = (cumsum(mask) - 1).masked_fill(mask == 0, 1)
-    int64_t c = 0;
-    for (int l = 0; l < L; ++l) {
-      c += mmrow[l];
-      pos[(int64_t)b * L + l] = mmrow[l] == 0 ? 1 : c - 1;
+    int64_t mc = 0;
+    for (int c0 = 0; c0 < L; c0 += kMergeThreads) {
+      const int l = c0 + t;
+      const int64_t m = l < L ? mmrow[l] : 0;
+      const int64_t c = mc + wg_incl_scan(m, lds, &tot);
+      mc += tot;
+      if (l < L) prow[l] = m == 0 ? 1 : c - 1;
     }
+    __syncthreads();
   }
 }
 
@@ -307,7 +347,7 @@ extern "C" int cullavo_merge_plan(const int64_t* ids, const int64_t* mask, int B
   CV_REQUIRE(B >= 0 && B <= 1024, CULLAVO_EINVAL, "B must be <= 1024");
   CV_REQUIRE(n_patches >= 1, CULLAVO_EINVAL, "n_patches");
   if (B == 0) return CULLAVO_OK;
-  merge_plan_k<<<1, 1024, 0, CV_STREAM(stream)>>>(ids, mask, B, S, L, image_token, n_patches, left_padding,
+  merge_plan_k<<<1, kMergeThreads, 0, CV_STREAM(stream)>>>(ids, mask, B, S, L, image_token, n_patches, left_padding,
                                                   text_dst, src, merged_mask, position_ids);
   return cullavo_check_launch("merge_plan");
 }

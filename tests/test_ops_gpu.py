@@ -553,3 +553,40 @@ def test_sumsq_deterministic_and_accurate():
     assert len(set(vals)) == 1
     ref = x.double().pow(2).sum().item()
     assert abs(vals[0] - ref) <= 1e-5 * ref
+
+
+@pytest.mark.parametrize("left", [False, True])
+def test_merge_plan_long_rows_bit_exact(left):
+    """rows longer than one 1024-wide scan chunk (S=1300 text ids, 576 patches per image, two
+    images in one row, padded rows): the chunk carries of the workgroup scans match the oracle"""
+    cfg = O.config_small_gpu()
+    B, S, P, D = 3, 1300, 576, 8
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(2, cfg.image_token_index - 1, (B, S), generator=g)
+    ids[0, 35] = cfg.image_token_index
+    ids[1, 10] = ids[1, 900] = cfg.image_token_index
+    ids[2, 1200] = cfg.image_token_index
+    mask = torch.ones(B, S, dtype=torch.long)
+    for b, n in ((0, 0), (1, 200), (2, 37)):
+        if n:
+            if left:
+                ids[b] = torch.cat([torch.full((n,), cfg.pad_token_id), ids[b, :S - n]])
+                mask[b, :n] = 0
+            else:
+                ids[b, S - n:] = cfg.pad_token_id
+                mask[b, S - n:] = 0
+    n_img = int((ids == cfg.image_token_index).sum())
+    emb = rnd((B, S, D), 97)
+    img = rnd((n_img, P, D), 98)
+    cfg_p = type("C", (), dict(pad_token_id=cfg.pad_token_id, image_token_index=cfg.image_token_index,
+                               ignore_index=-100, vision=type("V", (), dict(num_patches=P))()))()
+    r_emb, r_mask, _, r_pos = O.merge(img, emb, ids, mask, cfg_p)
+    L = r_emb.shape[1]
+    left_pad = not bool((ids[:, -1] == cfg.pad_token_id).sum())
+    assert left_pad == left
+    td, src, mm, pos = ops().merge_plan(ids.to(DEV), mask.to(DEV), L=L, image_token=cfg.image_token_index,
+                                       n_patches=P, left_padding=left_pad)
+    out = ops().row_gather2(src.reshape(-1), emb.to(DEV).reshape(-1, D), img.to(DEV).reshape(-1, D))
+    assert torch.equal(out.cpu().view(B, L, D), r_emb)
+    assert torch.equal(mm.cpu(), r_mask.long())
+    assert torch.equal(pos.cpu(), r_pos)
