@@ -42,17 +42,23 @@ class CullavoCausalLMOutputWithPast:
 
 class CuLLaVOModel(nn.Module):
     def __init__(self, config: CuLLaVOConfig, *, device="cuda", trainable: str = "full", init: str = "random",
-                 seed: int = 0, lora: LoraSettings | None = None):
+                 seed: int = 0, lora: LoraSettings | None = None, dtype=torch.bfloat16):
         """trainable: "full" | "reference" | "lora" | "none" (modeling.TRAINABLE_POLICIES); "lora"
-        adds the reference's peft adapters (lora.LoraSettings, default r=64, alpha=16, p=0.05)."""
+        adds the reference's peft adapters (lora.LoraSettings, default r=64, alpha=16, p=0.05).
+        dtype: torch.bfloat16 (production: the reference's bf16-cast model under bf16 autocast,
+        reference cullavo/load_cullavo.py:123-126) or torch.float32 (the parity mode: every
+        parameter, activation and kernel operand f32, nothing rounded to bf16)."""
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError(f"dtype {dtype}: bf16 (production) or float32 (parity mode)")
         super().__init__()
+        self.dtype = dtype
         if config.vision_config.hidden_act != "quick_gelu" or config.projector_hidden_act != "gelu":
             raise ValueError("CuLLaVO path: CLIP quick_gelu + projector gelu")
         self.config = config
         if trainable == "lora" and lora is None:
             lora = LoraSettings()
         self.lora_settings = lora if trainable == "lora" else None
-        self.arenas = build_arenas(config, device, trainable, lora=self.lora_settings)
+        self.arenas = build_arenas(config, device, trainable, dtype=dtype, lora=self.lora_settings)
         if init == "random":
             init_random_(self.arenas, seed)
         la = (self.arenas["lora"], self.lora_settings) if "lora" in self.arenas else None

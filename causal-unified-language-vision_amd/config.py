@@ -138,3 +138,14 @@ def tiny_gpu() -> CuLLaVOConfig:
         text_config=LlamaConfig(hidden_size=256, num_hidden_layers=2, num_attention_heads=2, intermediate_size=688,
                                 vocab_size=1024),
         image_token_index=1000, pad_token_id=1001)
+
+
+def config1() -> CuLLaVOConfig:
+    """BASELINE config 1: 224 px / 14, ViT d=64 x 3 layers x 4 heads (head
+    dim 16), LM 2 layers d=128 x 4 heads (head dim 32), ffn 344, vocab 1024."""
+    return CuLLaVOConfig(
+        vision_config=CLIPVisionConfig(image_size=224, patch_size=14, hidden_size=64, num_hidden_layers=3,
+                                       num_attention_heads=4, intermediate_size=256),
+        text_config=LlamaConfig(hidden_size=128, num_hidden_layers=2, num_attention_heads=4, intermediate_size=344,
+                                vocab_size=1024),
+        image_token_index=1000, pad_token_id=1001)

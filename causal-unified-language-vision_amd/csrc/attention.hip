@@ -612,14 +612,17 @@ extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64
                                 int64_t ldv, void* o, int64_t ldo, float* lse, int B, int H, int Lq, int Lk,
                                 int D, float scale, int causal, const int32_t* kv_start, int dtype,
                                 void* stream) {
-  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "attention is bf16 only");
-  CV_REQUIRE(D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 64 or 128");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "attention: bf16 / f32");
+  CV_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 16, 32, 64 or 128");
   CV_REQUIRE(!causal || Lq == Lk, CULLAVO_EINVAL, "causal attention needs Lq == Lk");
   CV_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0, CULLAVO_EINVAL, "token strides must be multiples of 8");
   CV_REQUIRE(ldq >= (int64_t)H * D && ldk >= (int64_t)H * D && ldv >= (int64_t)H * D && ldo >= (int64_t)H * D,
              CULLAVO_EINVAL, "token stride smaller than H*D");
   if (B == 0 || H == 0 || Lq == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
+  if (dtype == CULLAVO_DT_F32 || D < 64)  // f32 parity mode / config-1 head dims: attn_generic.hip
+    return cullavo_attn_generic_fwd(q, ldq, k, ldk, v, ldv, o, ldo, lse, B, H, Lq, Lk, D, scale, causal, kv_start,
+                                    dtype, s);
   const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v;
   u16* O = (u16*)o;
   if (D == 128)
@@ -634,14 +637,17 @@ extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64
                                 const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                                 int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                                 float scale, int causal, const int32_t* kv_start, int dtype, void* stream) {
-  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "attention is bf16 only");
-  CV_REQUIRE(D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 64 or 128");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "attention: bf16 / f32");
+  CV_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 16, 32, 64 or 128");
   CV_REQUIRE(!causal || Lq == Lk, CULLAVO_EINVAL, "causal attention needs Lq == Lk");
   CV_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 8 == 0 && lddo % 8 == 0 && lddq % 8 == 0 &&
                  lddk % 8 == 0 && lddv % 8 == 0,
              CULLAVO_EINVAL, "token strides must be multiples of 8");
   if (B == 0 || H == 0 || Lq == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
+  if (dtype == CULLAVO_DT_F32 || D < 64)
+    return cullavo_attn_generic_bwd(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, delta, dq, lddq, dk, lddk, dv,
+                                    lddv, B, H, Lq, Lk, D, scale, causal, kv_start, dtype, s);
   const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v, *O = (const u16*)o, *dO = (const u16*)dout;
   u16 *dQ = (u16*)dq, *dK = (u16*)dk, *dV = (u16*)dv;
 #define BWD4(DD, CC, QQ, KK) bwd_launch<DD, CC, QQ, KK>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)

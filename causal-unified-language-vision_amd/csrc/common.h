@@ -113,4 +113,17 @@ int cullavo_check_launch(const char* what);
 
 #define CV_STREAM(s) (reinterpret_cast<hipStream_t>(s))
 
+// gemm_f32.hip: cullavo_gemm_ex with f32_operands = 1
+int cullavo_gemm_f32_impl(const cullavo_gemm_desc& d, hipStream_t s);
+
+// attn_generic.hip: f32 storage / head dims 16-32 (dispatched from attention.hip)
+int cullavo_attn_generic_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                             void* o, int64_t ldo, float* lse, int B, int H, int Lq, int Lk, int D, float scale,
+                             int causal, const int32_t* ks, int dtype, hipStream_t s);
+int cullavo_attn_generic_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                             const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
+                             float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                             int B, int H, int Lq, int Lk, int D, float scale, int causal, const int32_t* ks,
+                             int dtype, hipStream_t s);
+
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -20,9 +20,9 @@ __global__ __launch_bounds__(256) void embedding_fwd_k(const int64_t* __restrict
 // One block per token position i. The block that holds the FIRST occurrence of ids[i] sums
 // every dout row with the same id in increasing position order (bitwise reproducible) and
 // writes that table row once; later occurrences exit.
-template <typename TT>
+template <typename TT, typename TD>
 __global__ __launch_bounds__(256) void embedding_bwd_k(const int64_t* __restrict__ ids, int64_t n,
-                                                       const u16* __restrict__ dout, int64_t vocab,
+                                                       const TD* __restrict__ dout, int64_t vocab,
                                                        int64_t dim, TT* __restrict__ dtable, float beta) {
   __shared__ int64_t first;
   __shared__ int match[256];
@@ -91,13 +91,13 @@ __global__ __launch_bounds__(256) void embedding_bwd_k(const int64_t* __restrict
 }
 
 // ---- CLIP patch embedding (tf:clip/modeling_clip.py:202-218) -------------------------------
-template <typename TP>
+template <typename TP, typename TO>
 __global__ __launch_bounds__(256) void im2col_k(const TP* __restrict__ pix, int C, int H, int W, int patch,
-                                                int gw, int P, u16* __restrict__ out, int64_t kpad) {
+                                                int gw, int P, TO* __restrict__ out, int64_t kpad) {
   const int64_t r = blockIdx.x;  // output row in [B*(1+P)]
   const int b = (int)(r / (1 + P));
   const int t = (int)(r % (1 + P));
-  u16* o = out + r * kpad;
+  TO* o = out + r * kpad;
   const int kreal = C * patch * patch;
   for (int64_t c = threadIdx.x; c < kpad; c += 256) {
     float v = 0.f;
@@ -107,14 +107,14 @@ __global__ __launch_bounds__(256) void im2col_k(const TP* __restrict__ pix, int 
       const int i = rem / patch, j = rem % patch;
       v = Elt<TP>::ld(pix, (((int64_t)b * C + ch) * H + (py * patch + i)) * W + px * patch + j);
     }
-    o[c] = f2bf(v);  // the reference casts pixel_values to the conv weight dtype (bf16) first
+    Elt<TO>::st(o, c, v);  // the reference casts pixel_values to the conv weight dtype first
   }
 }
 
-template <int NCH>
-__global__ __launch_bounds__(256) void vision_embed_ln_k(const u16* __restrict__ x, const u16* __restrict__ cls,
-                                                         const u16* __restrict__ pos, const u16* __restrict__ w,
-                                                         const u16* __restrict__ b, u16* __restrict__ y,
+template <typename TE, int NCH>
+__global__ __launch_bounds__(256) void vision_embed_ln_k(const TE* __restrict__ x, const TE* __restrict__ cls,
+                                                         const TE* __restrict__ pos, const TE* __restrict__ w,
+                                                         const TE* __restrict__ b, TE* __restrict__ y,
                                                          int64_t rows, int T, int cols, float eps) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -133,10 +133,10 @@ __global__ __launch_bounds__(256) void vision_embed_ln_k(const u16* __restrict__
         float cv[8];
         load8(cls + col, cv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = round_bf(cv[j] + pv[j]);
+        for (int j = 0; j < 8; ++j) v[c][j] = Elt<TE>::rnd(cv[j] + pv[j]);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = round_bf(v[c][j] + pv[j]);
+        for (int j = 0; j < 8; ++j) v[c][j] = Elt<TE>::rnd(v[c][j] + pv[j]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[c][j];
@@ -230,7 +230,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_plan_k(
         if (img) {
           text_dst[(int64_t)b * S + s] = -1;
         } else {
-          text_dst[(int64_t)b * S + s] = dst;
+          // flattened merged row (b * L + dst) or -1 when the slot falls outside the row
+          text_dst[(int64_t)b * S + s] = (dst >= 0 && dst < L) ? (int64_t)b * L + dst : -1;
           if (dst >= 0 && dst < L) {
             srow[dst] = (int64_t)b * S + s;
             mmrow[dst] = mr ? mr[s] : 1;
@@ -286,57 +287,72 @@ __global__ __launch_bounds__(256) void row_gather2_k(const int64_t* __restrict__
 
 extern "C" int cullavo_embedding_fwd(const int64_t* ids, int64_t n, const void* table, int64_t vocab,
                                      int64_t dim, void* out, int dtype, void* stream) {
-  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "bf16 only");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "bf16 / f32");
   CV_REQUIRE(dim % 8 == 0, CULLAVO_EINVAL, "dim must be a multiple of 8");
   if (n == 0) return CULLAVO_OK;
-  embedding_fwd_k<<<(unsigned)n, 256, 0, CV_STREAM(stream)>>>(ids, (const u16*)table, vocab, dim, (u16*)out);
+  // a row copy: f32 rows move as twice as many 16-bit units
+  const int64_t units = dtype == CULLAVO_DT_F32 ? dim * 2 : dim;
+  embedding_fwd_k<<<(unsigned)n, 256, 0, CV_STREAM(stream)>>>(ids, (const u16*)table, vocab, units, (u16*)out);
   return cullavo_check_launch("embedding_fwd");
 }
 
 extern "C" int cullavo_embedding_bwd(const int64_t* ids, int64_t n, const void* dout, int64_t vocab,
                                      int64_t dim, void* dtable, int table_dtype, float beta, int dtype,
                                      void* stream) {
-  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "bf16 only");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "bf16 / f32");
   CV_REQUIRE(dim % 8 == 0 && dim <= 8192, CULLAVO_EINVAL, "dim must be a multiple of 8 and <= 8192");
   if (n == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
-  if (table_dtype == CULLAVO_DT_BF16)
-    embedding_bwd_k<u16><<<(unsigned)n, 256, 0, s>>>(ids, n, (const u16*)dout, vocab, dim, (u16*)dtable, beta);
-  else
-    embedding_bwd_k<float><<<(unsigned)n, 256, 0, s>>>(ids, n, (const u16*)dout, vocab, dim, (float*)dtable, beta);
+#define EBW(TT, TD) embedding_bwd_k<TT, TD><<<(unsigned)n, 256, 0, s>>>(ids, n, (const TD*)dout, vocab, dim, (TT*)dtable, beta)
+  if (dtype == CULLAVO_DT_BF16) {
+    if (table_dtype == CULLAVO_DT_BF16) EBW(u16, u16);
+    else EBW(float, u16);
+  } else {
+    if (table_dtype == CULLAVO_DT_BF16) EBW(u16, float);
+    else EBW(float, float);
+  }
+#undef EBW
   return cullavo_check_launch("embedding_bwd");
 }
 
 extern "C" int cullavo_im2col_patches(const void* pixels, int pix_dtype, int B, int C, int H, int W,
-                                      int patch, void* out, int64_t kpad, void* stream) {
+                                      int patch, void* out, int64_t kpad, int out_dtype, void* stream) {
   CV_REQUIRE(H % patch == 0 && W % patch == 0, CULLAVO_EINVAL, "image size must be a multiple of patch");
   CV_REQUIRE(kpad >= (int64_t)C * patch * patch, CULLAVO_EINVAL, "kpad too small");
   const int gw = W / patch, P = (H / patch) * gw;
   const int64_t rows = (int64_t)B * (1 + P);
   if (rows == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
-  if (pix_dtype == CULLAVO_DT_F32)
-    im2col_k<float><<<(unsigned)rows, 256, 0, s>>>((const float*)pixels, C, H, W, patch, gw, P, (u16*)out, kpad);
-  else
-    im2col_k<u16><<<(unsigned)rows, 256, 0, s>>>((const u16*)pixels, C, H, W, patch, gw, P, (u16*)out, kpad);
+#define I2C(TP, TO) im2col_k<TP, TO><<<(unsigned)rows, 256, 0, s>>>((const TP*)pixels, C, H, W, patch, gw, P, (TO*)out, kpad)
+  if (out_dtype == CULLAVO_DT_BF16) {
+    if (pix_dtype == CULLAVO_DT_F32) I2C(float, u16);
+    else I2C(u16, u16);
+  } else {
+    if (pix_dtype == CULLAVO_DT_F32) I2C(float, float);
+    else I2C(u16, float);
+  }
+#undef I2C
   return cullavo_check_launch("im2col_patches");
 }
 
 extern "C" int cullavo_vision_embed_ln(const void* x, const void* cls, const void* pos, const void* w,
                                        const void* b, void* y, int B, int T, int64_t dim, float eps,
-                                       void* stream) {
+                                       int dtype, void* stream) {
   CV_REQUIRE(dim % 8 == 0 && dim <= 8192, CULLAVO_EINVAL, "dim");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "bf16 / f32");
   const int64_t rows = (int64_t)B * T;
   if (rows == 0) return CULLAVO_OK;
   hipStream_t s = CV_STREAM(stream);
   const int nb = (int)cdiv(rows, 4);
-#define VEL(N) vision_embed_ln_k<N><<<nb, 256, 0, s>>>((const u16*)x, (const u16*)cls, (const u16*)pos, (const u16*)w, (const u16*)b, (u16*)y, rows, T, (int)dim, eps)
+#define VEL1(T_, N) vision_embed_ln_k<T_, N><<<nb, 256, 0, s>>>((const T_*)x, (const T_*)cls, (const T_*)pos, (const T_*)w, (const T_*)b, (T_*)y, rows, T, (int)dim, eps)
+#define VEL(N) do { if (dtype == CULLAVO_DT_F32) VEL1(float, N); else VEL1(u16, N); } while (0)
   if (dim <= 512) VEL(1);
   else if (dim <= 1024) VEL(2);
   else if (dim <= 2048) VEL(4);
   else if (dim <= 4096) VEL(8);
   else VEL(16);
 #undef VEL
+#undef VEL1
   return cullavo_check_launch("vision_embed_ln");
 }
 
@@ -354,9 +370,10 @@ extern "C" int cullavo_merge_plan(const int64_t* ids, const int64_t* mask, int B
 
 extern "C" int cullavo_row_gather2(const int64_t* src, int64_t rows, const void* a, int64_t n_a,
                                    const void* b, int64_t dim, void* out, int dtype, void* stream) {
-  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "bf16 only");
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "bf16 / f32");
   CV_REQUIRE(dim % 8 == 0, CULLAVO_EINVAL, "dim must be a multiple of 8");
   if (rows == 0) return CULLAVO_OK;
-  row_gather2_k<<<(unsigned)rows, 256, 0, CV_STREAM(stream)>>>(src, (const u16*)a, n_a, (const u16*)b, dim, (u16*)out);
+  const int64_t units = dtype == CULLAVO_DT_F32 ? dim * 2 : dim;  // row copy in 16-bit units
+  row_gather2_k<<<(unsigned)rows, 256, 0, CV_STREAM(stream)>>>(src, (const u16*)a, n_a, (const u16*)b, units, (u16*)out);
   return cullavo_check_launch("row_gather2");
 }

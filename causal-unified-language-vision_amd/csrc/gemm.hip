@@ -1071,6 +1071,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   CV_REQUIRE(d.drop_operand == 0 || (d.drop_p >= 0.f && d.drop_p < 1.f), CULLAVO_EINVAL, "drop_p must be in [0, 1)");
   CV_REQUIRE(d.drop_operand != 1 || a_layout == 0, CULLAVO_EUNSUPPORTED, "dropout on A needs a_layout 0");
   CV_REQUIRE(d.drop_operand != 2 || b_layout == 1, CULLAVO_EUNSUPPORTED, "dropout on B needs b_layout 1");
+  if (d.f32_operands) return cullavo_gemm_f32_impl(d, CV_STREAM(stream));  // gemm_f32.hip
   if (M == 0 || N == 0) return CULLAVO_OK;
   const int64_t tm = cdiv(M, BM), tn = cdiv(N, BN);
   CV_REQUIRE(tm * tn < (1ll << 31), CULLAVO_EINVAL, "too many tiles");

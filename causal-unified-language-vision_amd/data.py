@@ -29,8 +29,8 @@ def synthetic_batch(cfg: CuLLaVOConfig, batch: int, text_len: int = 513, image_c
     mask = torch.ones_like(ids)
     pix = torch.randn(batch, v.num_channels, v.image_size, v.image_size, generator=g, device=device)
     L = text_len + P - 1
-    if label_from is None:
-        label_from = min(L - 1, image_col + P + 40)
+    if label_from is None:  # -100 for merged positions < image_col + P (611 at 7B)
+        label_from = min(L - 1, image_col + P)
     labels = torch.full((batch, L), cfg.ignore_index, dtype=torch.long, device=device)
     labels[:, label_from:] = torch.randint(2, cfg.image_token_index, (batch, L - label_from), generator=g,
                                            device=device)

@@ -338,6 +338,9 @@ class HeadLossFn(torch.autograd.Function):
         out = ops.ce_reduce(row_loss, targets, ignore_index)
         ctx.lm = lm
         ctx.ignore = ignore_index
+        # logits are an output for callers that use them; when nothing downstream does (the
+        # training step), autograd passes None instead of a materialised zero [T, V] gradient
+        ctx.set_materialize_grads(False)
         ctx.saved = (h, x, rstd, logits, targets, lse, out)
         ctx.stats = out  # [loss, count, 1/count] on device (no host sync)
         return out[0].clone(), logits

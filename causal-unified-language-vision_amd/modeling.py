@@ -271,6 +271,18 @@ class CLIPVisionTransformer(nn.Module):
         self.post_layernorm = LayerNorm(P[prefix + "post_layernorm.weight"], P[prefix + "post_layernorm.bias"],
                                         cfg.layer_norm_eps)
         self.kpad = int(math.ceil(cfg.num_channels * cfg.patch_size ** 2 / 64) * 64)
+        self._arena = arena
+        self._wpad = None  # (arena state it was packed from, [d, kpad] patch weight)
+
+    def packed_patch_weight(self):
+        """Conv2d weight [d, C, p, p] as a K-padded GEMM operand [d, kpad], packed once and
+        re-packed only when the vision arena was written since (a trainable tower, a load)."""
+        st = self._arena._state()
+        if self._wpad is None or self._wpad[0] != st:
+            w = self.embeddings.patch_embedding.weight
+            wk = w.detach().reshape(w.shape[0], -1)
+            self._wpad = (st, F.pad(wk, (0, self.kpad - wk.shape[1])).contiguous())
+        return self._wpad[1]
 
     def embed(self, pixel_values):
         """patch conv (im2col + MFMA GEMM) + CLS + positions + pre_layrnorm -> [B*T, d]."""
@@ -281,11 +293,8 @@ class CLIPVisionTransformer(nn.Module):
                              f"match model ({cfg.image_size}*{cfg.image_size}).")
         if pixel_values.dtype not in (torch.float32, torch.bfloat16):
             pixel_values = pixel_values.float()
-        patches = ops.im2col_patches(pixel_values, cfg.patch_size, self.kpad)
-        w = self.embeddings.patch_embedding.weight
-        wk = w.detach().reshape(w.shape[0], -1)
-        wpad = F.pad(wk, (0, self.kpad - wk.shape[1])).contiguous()  # weight packing (frozen path)
-        x = ops.linear(patches, wpad)
+        patches = ops.im2col_patches(pixel_values, cfg.patch_size, self.kpad, dtype=self._arena.dtype)
+        x = ops.linear(patches, self.packed_patch_weight())
         T = cfg.num_patches + 1
         return ops.vision_embed_ln(x, self.embeddings.class_embedding, self.embeddings.position_embedding.weight,
                                    self.pre_layrnorm.weight, self.pre_layrnorm.bias, B=B, T=T,

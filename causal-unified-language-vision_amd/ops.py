@@ -79,6 +79,9 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
          alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
          beta: float = 0.0):
     _dev(A, B, C, bias, preact, residual)
+    if A.dtype == torch.float32:  # f32 parity mode: every operand f32 (cullavo_gemm_ex f32_operands)
+        return gemm_ex(a_layout, b_layout, M, N, K, A, lda, B, ldb, C, ldc, alpha=alpha, bias=bias, act=act,
+                       preact=preact, residual=residual, ldr=ldr, beta=beta, split_k=False)
     traced = _TRACE["key"] is not None and _TRACE["key"] == (M, N, K, a_layout, b_layout)
     if traced:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -101,7 +104,8 @@ class GemmDesc(ctypes.Structure):
                 ("act", ctypes.c_int), ("preact", ctypes.c_void_p), ("residual", ctypes.c_void_p),
                 ("ldr", ctypes.c_int64), ("beta", ctypes.c_float), ("addend", ctypes.c_void_p),
                 ("ld_addend", ctypes.c_int64), ("drop_operand", ctypes.c_int), ("drop_p", ctypes.c_float),
-                ("drop_seed", ctypes.c_uint64), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64)]
+                ("drop_seed", ctypes.c_uint64), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+                ("f32_operands", ctypes.c_int)]
 
 
 DROP_NONE, DROP_A, DROP_B, DROP_OUT = 0, 1, 2, 3
@@ -115,11 +119,15 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
     """cullavo_gemm_ex: gemm() plus the LoRA addend, dropout masks and split-K (see the header).
     The split-K workspace comes from torch's caching allocator (kernels never allocate)."""
     _dev(A, B, C, bias, preact, residual, addend)
+    f32 = A.dtype == torch.float32
+    for t in (B, C, bias, preact, residual, addend):
+        if f32 and t is not None and t.dtype != torch.float32:
+            raise TypeError("gemm: f32 operands need every operand and the output in f32")
     d = GemmDesc(a_layout, b_layout, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _dt(C), float(alpha),
                  _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _ptr(addend), ld_addend,
-                 drop_operand, float(drop_p), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, None, 0)
+                 drop_operand, float(drop_p), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, None, 0, int(f32))
     ws = None
-    if split_k:
+    if split_k and not f32:
         nbytes = lib().cullavo_gemm_workspace(ctypes.addressof(d))
         if nbytes:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=C.device)
@@ -355,13 +363,13 @@ def embedding_bwd(ids, dout, dtable, *, beta: float = 0.0):
     return dtable
 
 
-def im2col_patches(pixels, patch: int, kpad: int):
+def im2col_patches(pixels, patch: int, kpad: int, dtype=torch.bfloat16):
     _dev(pixels)
     B, C, H, W = pixels.shape
     P = (H // patch) * (W // patch)
-    out = torch.empty((B * (1 + P), kpad), dtype=torch.bfloat16, device=pixels.device)
+    out = torch.empty((B * (1 + P), kpad), dtype=dtype, device=pixels.device)
     pixels = pixels.contiguous()
-    call("im2col_patches", _ptr(pixels), _dt(pixels), B, C, H, W, patch, _ptr(out), kpad, _stream())
+    call("im2col_patches", _ptr(pixels), _dt(pixels), B, C, H, W, patch, _ptr(out), kpad, _dt(out), _stream())
     return out
 
 
@@ -369,7 +377,7 @@ def vision_embed_ln(x, cls, pos, w, b, *, B: int, T: int, eps: float):
     _dev(x, cls, pos, w, b)
     y = torch.empty_like(x)
     call("vision_embed_ln", _ptr(x), _ptr(cls), _ptr(pos), _ptr(w), _ptr(b), _ptr(y), B, T, x.shape[1],
-         float(eps), _stream())
+         float(eps), _dt(x), _stream())
     return y
 
 

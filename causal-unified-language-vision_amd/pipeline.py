@@ -14,10 +14,10 @@ import torch
 from torch import nn
 
 from .arch_cullavo import CuLLaVOModel
-from .config import CuLLaVOConfig, llava_1_5_13b, llava_1_5_7b, tiny_gpu
+from .config import CuLLaVOConfig, config1, llava_1_5_13b, llava_1_5_7b, tiny_gpu
 from .data import SyntheticLoader
 
-MODEL_CONFIGS = {"llava-1.5-7b": llava_1_5_7b, "llava-1.5-13b": llava_1_5_13b, "tiny": tiny_gpu}
+MODEL_CONFIGS = {"llava-1.5-7b": llava_1_5_7b, "llava-1.5-13b": llava_1_5_13b, "tiny": tiny_gpu, "config1": config1}
 _REGISTRY = {}
 
 

@@ -102,6 +102,9 @@ typedef struct {
   uint64_t drop_seed;
   void* workspace;          /* nullable: split-K f32 partials (size: cullavo_gemm_workspace) */
   int64_t workspace_bytes;
+  int f32_operands;         /* 0 (default): A, B, bias, residual, preact, addend bf16;
+                               1: every operand and C f32, nothing rounded (the f32 parity
+                               mode: an exact f32 MFMA chain, v_mfma_f32_16x16x4_f32) */
 } cullavo_gemm_desc;
 int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream);
 /* sizeof(cullavo_gemm_desc) as compiled into the library (binding check) */
@@ -248,14 +251,16 @@ int cullavo_embedding_bwd(const int64_t* ids, int64_t n, const void* dout, int64
  * bf16 by pix_dtype) -> patches [B*(1+P), kpad] bf16, row b*(1+P) (the CLS slot) all zeros,
  * column order (c, i, j) like Conv2d.weight.reshape(out, -1), zero pad to kpad. */
 int cullavo_im2col_patches(const void* pixels, int pix_dtype, int B, int C, int H, int W,
-                           int patch, void* out, int64_t kpad, void* stream);
-/* x[b,t] += (t==0 ? cls : 0) + pos[t] then LayerNorm (pre_layrnorm); x: [B*T, dim] bf16 */
+                           int patch, void* out, int64_t kpad, int out_dtype, void* stream);
+/* x[b,t] += (t==0 ? cls : 0) + pos[t] then LayerNorm (pre_layrnorm); x: [B*T, dim] (dtype;
+ * bf16 rounds the embedding sum like the reference's bf16 add, f32 keeps it exact) */
 int cullavo_vision_embed_ln(const void* x, const void* cls, const void* pos, const void* w,
                             const void* b, void* y, int B, int T, int64_t dim, float eps,
-                            void* stream);
+                            int dtype, void* stream);
 /* The llava _merge_input_ids_with_image_features index plan (transformers ~4.37, called at
  * reference cullavo/arch_cullavo.py:600-602). ids/mask: [B,S]; per text token its merged
- * row (text_dst [B,S], -1 for image tokens), per merged row its source (src [B,L]: text row
+ * row, flattened over the batch (text_dst [B,S] = b*L + position, -1 for image tokens; the
+ * backward gathers the text gradient with it), per merged row its source (src [B,L]: text row
  * b*S+s, or B*S + image row, or -1 for zero fill), merged mask [B,L] and position_ids [B,L].
  * n_patches = image feature rows per image. Returns CULLAVO_EINVAL when the image-token count
  * does not match n_images (the reference's ValueError). img_count/left_pad from host. */

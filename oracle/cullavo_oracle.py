@@ -3,8 +3,14 @@
 This module is the checker the parity tests, ``__graft_entry__.smoke()`` and ``bench.py``'s
 ``cpu_baseline`` leg compare against; the product path (``cullavo_amd``) never imports it.
 
-It is a plain PyTorch fp32 restatement (torch autograd supplies the backward) of what the
-reference executes for one training step:
+It is a plain PyTorch restatement (torch autograd supplies the backward) of what the
+reference executes for one training step. With fp32 weights it is the reference's fp32 path
+(pinned below); with bf16 weights (``to_bf16``) it is the bf16-faithful mode: every module
+output, residual add and norm output rounds to bf16 where the reference's bf16-cast model
+under bf16 autocast rounds (reference cullavo/load_cullavo.py:123-126,
+configs/accel/ddp_accel.yaml:8), RMSNorm keeps f32 statistics and casts before the weight
+(tf:llama :63-67), RoPE casts its f32 cos/sin to bf16 (:121-125), attention keeps FA2's f32
+scores/softmax with bf16 P, and the loss upcasts the bf16 logits to f32 (4.37):
 
 * ``forward``          — reference cullavo/arch_cullavo.py:546-677 (CuLLaVOModel.forward):
                           embed :582, vision tower :586, feature select :588-597,
@@ -184,6 +190,11 @@ def make_weights(cfg: CuLLaVOCfg, seed: int = 0) -> dict[str, torch.Tensor]:
     return {k: init_tensor(k, shp, kind, seed) for k, (shp, kind) in weight_shapes(cfg).items()}
 
 
+def to_bf16(W: dict[str, torch.Tensor]) -> dict[str, torch.Tensor]:
+    """The bf16 cast of every parameter (reference cullavo/load_cullavo.py:123-126)."""
+    return {k: v.detach().to(torch.bfloat16) for k, v in W.items()}
+
+
 # ---------------------------------------------------------------------------------------------
 # synthetic inputs (SURVEY.md §8(d) config 1 / config 3 recipes)
 # ---------------------------------------------------------------------------------------------
@@ -216,10 +227,11 @@ def make_inputs(cfg: CuLLaVOCfg, batch: int, text_len: int, image_col: int, seed
 # ops
 # ---------------------------------------------------------------------------------------------
 def rmsnorm(x, w, eps):
-    """tf:models/llama/modeling_llama.py:53-70"""
+    """tf:models/llama/modeling_llama.py:53-70: f32 statistics, then weight * x.to(input dtype)
+    (a no-op cast in f32; the bf16 rounding point in the bf16-faithful mode)"""
     xf = x.float()
     var = xf.pow(2).mean(-1, keepdim=True)
-    return w * (xf * torch.rsqrt(var + eps))
+    return w * (xf * torch.rsqrt(var + eps)).to(x.dtype)
 
 
 def layernorm(x, w, b, eps):
@@ -241,7 +253,9 @@ def rotate_half(x):
 
 
 def apply_rope(x, cos, sin):
-    """x [B,H,L,D], cos/sin [B,L,D] (tf:models/llama/modeling_llama.py:138-160)"""
+    """x [B,H,L,D], cos/sin [B,L,D] (tf:models/llama/modeling_llama.py:138-160); cos/sin are
+    computed in f32 and cast to the activation dtype (:121-125)"""
+    cos, sin = cos.to(x.dtype), sin.to(x.dtype)
     return x * cos[:, None] + rotate_half(x) * sin[:, None]
 
 
@@ -249,7 +263,9 @@ def attention(q, k, v, scale, allowed=None):
     """eager attention, fp32 softmax (tf:models/llama/modeling_llama.py:191-214,
     tf:models/clip/modeling_clip.py eager path); q/k/v [B,H,L,D]; allowed [B,1|H,Lq,Lk] bool.
     Rows with no allowed key return zeros."""
-    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    # scores and softmax in f32 (the flash kernels' and FA2's arithmetic), P cast to the value
+    # dtype for the PV product: with f32 inputs this is the plain fp32 eager path
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if allowed is not None:
         s = s.masked_fill(~allowed, float("-inf"))
         p = torch.softmax(s.float(), dim=-1)
@@ -465,6 +481,8 @@ def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, la
     strategy = cfg.vision_feature_select_strategy if vision_feature_select_strategy is None \
         else vision_feature_select_strategy
     inputs_embeds = W["language_model.model.embed_tokens.weight"][input_ids]
+    # bf16-faithful mode (bf16 weights): the processor's f32 pixels meet the bf16 conv weight
+    pixel_values = pixel_values.to(W["vision_tower.vision_model.embeddings.patch_embedding.weight"].dtype)
     # image_outputs.hidden_states[vision_feature_layer]: only layers up to that index are needed
     n_needed = needed_vision_layers(cfg, layer)
     hs = vision_hidden_states(pixel_values, W, cfg.vision, n_needed, vision_lora)

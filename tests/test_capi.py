@@ -32,7 +32,7 @@ def test_validation_errors_surface_without_gpu():
         _lib.call("gemm", 0, 0, 16, 16, 12, None, 12, None, 12, None, 16, 1, 1.0, None, 0, None, None, 0, 0.0, None)
     with pytest.raises(ValueError, match="head_dim"):
         _lib.call("rope", None, 128, None, 128, None, 4, 1, 1, 12, 10000.0, 0, 1, None)
-    with pytest.raises(Exception, match="head_dim must be 64 or 128"):
+    with pytest.raises(Exception, match="head_dim must be 16, 32, 64 or 128"):
         _lib.call("attn_fwd", None, 96, None, 96, None, 96, None, 96, None, 1, 1, 4, 4, 96, 1.0, 1, None, 1, None)
 
 

@@ -55,8 +55,13 @@ def tile_mode(request):
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES + [(520, 264, 8704), (8, 1032, 136)])
 @pytest.mark.parametrize("al,bl", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_layouts(M, N, K, al, bl, tile_mode):
-    if al == 1 and M % 8:
-        pytest.skip("a_layout 1 needs M % 8 == 0")
+    if al == 1 and M % 8:  # unsupported shape: rejected on the host with the reference-style error
+        A = torch.empty((K, M), dtype=BF, device=DEV)
+        B = torch.empty((N, K) if bl == 0 else (K, N), dtype=BF, device=DEV)
+        C = torch.empty((M, N), dtype=BF, device=DEV)
+        with pytest.raises(ValueError, match="M must be a multiple of 8"):
+            ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N)
+        return
     A = rnd((M, K), 1)
     B = rnd((N, K), 2)
     ref = A.float() @ B.float().T
@@ -382,6 +387,12 @@ def test_merge_plan_bit_exact(pad_tail, left):
     assert torch.equal(out.cpu().view(2, L, D), r_emb)
     assert torch.equal(mm.cpu(), r_mask.long())
     assert torch.equal(pos.cpu(), r_pos)
+    # backward plan: the text gradient is the merged-row gradient gathered through text_dst
+    emb_r = emb.clone().requires_grad_(True)
+    G = rnd((2, L, D), 97)
+    O.merge(img, emb_r, ids, mask, cfg)[0].backward(G)
+    dtext = ops().row_gather2(td.reshape(-1), G.to(DEV).reshape(-1, D), None)
+    assert torch.equal(dtext.cpu().view(2, 40, D), emb_r.grad)
 
 
 def test_ce_fwd_bwd():
