@@ -99,6 +99,11 @@ class CuLLaVOModel(nn.Module):
         return step2_process(batched_inputs, processor, device, self.config.ignore_index,
                              self.config.vision_config.image_size)
 
+    def step2_preprocess(self, batched_inputs, processor, device, **kw):
+        """reference cullavo/arch_cullavo.py:341-395 (prompting.step2_preprocess, on generate())"""
+        from .prompting import step2_preprocess
+        return step2_preprocess(self, batched_inputs, processor, device, **kw)
+
     def eval_process(self, images, aux_prompt=None, prompt=None, processor=None, device=None):
         from .prompting import eval_process
         return eval_process(images, aux_prompt, prompt, processor, device, self.config.ignore_index)
@@ -161,9 +166,10 @@ class CuLLaVOModel(nn.Module):
             B, S = input_ids.shape
             inputs_embeds = self.get_input_embeddings()(input_ids)  # :582
             if pixel_values is not None and S != 1:
+                stats = self._merge_stats_async(input_ids)  # read back while the tower runs
                 image_features = self._image_features(pixel_values, vision_feature_layer, strategy)  # :586-599
                 inputs_embeds, attention_mask, position_ids = self._merge(image_features, inputs_embeds, input_ids,
-                                                                          attention_mask)  # :600-602
+                                                                          attention_mask, stats)  # :600-602
                 if labels is None:  # :603-604
                     labels = torch.full_like(attention_mask, cfg.ignore_index).to(torch.long)
         B, L, d = inputs_embeds.shape
@@ -233,9 +239,12 @@ class CuLLaVOModel(nn.Module):
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
         n_img = int((input_ids == cfg.image_token_index).sum(-1).max()) if pixel_values is not None else 0
-        L0 = S + n_img * (cfg.vision_config.num_patches - 1)
+        strategy = kw.get("vision_feature_select_strategy", cfg.vision_feature_select_strategy)
+        # image feature rows per <image> token: the patches, plus CLS under "full" (:588-597)
+        n_feat = cfg.vision_config.num_patches + (1 if strategy == "full" else 0)
+        L0 = S + n_img * (n_feat - 1)
         out = self._forward_cached(input_ids, pixel_values, attention_mask, None, None, None,
-                                   cfg.vision_feature_layer, cfg.vision_feature_select_strategy, None, True,
+                                   cfg.vision_feature_layer, strategy, None, True,
                                    max_len=L0 + max_new_tokens)
         cache = out.past_key_values
         logits = out.logits[:, -1]
@@ -273,16 +282,30 @@ class CuLLaVOModel(nn.Module):
             raise ValueError(f"Unexpected select feature strategy: {self.config.vision_feature_select_strategy}")
         return self.multi_modal_projector(feats)
 
-    def _merge(self, image_features, inputs_embeds, input_ids, attention_mask):
+    def _merge_stats_async(self, input_ids):
+        """The three integers that size the merge (max image tokens per row, total image
+        tokens, rows ending in <pad>), reduced on the GPU and copied to pinned host memory
+        without waiting: the copy completes long before the vision tower enqueued behind it,
+        so the host read in _merge does not drain the GPU queue."""
+        cfg = self.config
+        is_img = input_ids == cfg.image_token_index
+        st = torch.stack([is_img.sum(-1).max(), is_img.sum(), (input_ids[:, -1] == cfg.pad_token_id).sum()])
+        host = torch.empty(3, dtype=st.dtype, pin_memory=True)
+        host.copy_(st, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
+    def _merge(self, image_features, inputs_embeds, input_ids, attention_mask, stats=None):
         """transformers ~4.37 _merge_input_ids_with_image_features on the merge_plan kernel.
         One small device->host read (image-token counts, left-padding flag) sizes the output,
         as the reference's .max() / torch.where do."""
         cfg = self.config
         n_img, P, d = image_features.shape
         B, S = input_ids.shape
-        is_img = input_ids == cfg.image_token_index
-        stats = torch.stack([is_img.sum(-1).max(), is_img.sum(), (input_ids[:, -1] == cfg.pad_token_id).sum()]).cpu()
-        n_max, n_total, n_pad_last = (int(x) for x in stats)
+        host, ev = stats if stats is not None else self._merge_stats_async(input_ids)
+        ev.synchronize()
+        n_max, n_total, n_pad_last = (int(x) for x in host.tolist())
         if n_total != n_img:
             raise ValueError(f"The input provided to the model are wrong. The number of image tokens is {n_total} "
                              f"while the number of image given to the model is {n_img}. This prevents correct "

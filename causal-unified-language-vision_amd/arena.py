@@ -40,6 +40,9 @@ class ParamArena:
         self.trainable = trainable
         self.grad_flat = None
         self._written: set[str] = set()
+        # keys with no gradient this cycle (zeroed by finalize_grads): the optimizer skips them
+        # like torch.optim.AdamW skips parameters whose .grad is None
+        self.skipped: set[str] = set()
         self._write_hooks: list = []  # called with the keys whose gradient write is enqueued
         self._writes = 0  # writes torch's version counter cannot see (kernels on raw pointers)
         self._kmajor: dict[str, list] = {}  # first_key -> [buffer [K, N], state made from, pending event]
@@ -155,14 +158,22 @@ class ParamArena:
                 self.grad_flat[o:o + n].zero_()
             self._attach_grads()
         self._written = set()
+        self.skipped = set()
 
     def finalize_grads(self):
-        """Zero the gradient of every parameter that received no write this cycle."""
+        """Zero the gradient of every parameter that received no write this cycle, record it as
+        skipped for this cycle's optimizer step and commit it (so DP buckets holding it can be
+        reduced: their all-reduce is issued behind the zeroing)."""
         if self.trainable:
+            zeroed = []
             for k, (o, n, _) in self.offsets.items():
                 if k not in self._written:
                     self.grad_flat[o:o + n].zero_()
                     self._written.add(k)
+                    zeroed.append(k)
+            self.skipped.update(zeroed)
+            if zeroed:
+                self.commit(zeroed)
 
 
 def grad_slot(p: nn.Parameter, span=None):

@@ -20,9 +20,21 @@
      <save_dir>/epoch{e}/cullavo/multi_modal_projector.pt   {linear_1.weight, ...}
      <save_dir>/epoch{e}/cullavo/lm_head.pt                 {weight}
      <save_dir>/epoch{e}/cullavo/embed_tokens.pt            {weight}
-   Adapter keys are relative to the tower (vision_model.encoder.layers.N.self_attn.q_proj
-   .lora_A.weight, model.layers.N....) with the adapter name dropped, as peft's
-   get_peft_model_state_dict writes them; the loader accepts them with or without it.
+   Adapter keys are what the reference's `<tower>.save_pretrained(path)` writes for a model
+   carrying transformers-PEFT adapters (reference modeling/BaseModel.py:41-42 on towers set up
+   with add_adapter, cullavo/load_cullavo.py:111-112): transformers' save_pretrained
+   (tf:modeling_utils.py:3410-3422, save_peft_format=True by default) takes
+   get_adapter_state_dict (tf:integrations/peft.py:537-564 -> peft get_peft_model_state_dict,
+   which drops the adapter name) and prefixes `base_model.model.`:
+     base_model.model.vision_model.encoder.layers.N.self_attn.q_proj.lora_A.weight
+     base_model.model.model.layers.N.self_attn.q_proj.lora_A.weight
+   The loader accepts that form, the unprefixed form and the adapter-named parameter names.
+   (peft itself is not importable here: the key form is pinned to the transformers code above,
+   the peft step is restated -- parity of the adapter file layout is otherwise unpinned.)
+   Trainable arenas the reference never trains (this build's full fine-tune recipe) are saved
+   too, in the tower's own safetensors layout, so no trained weight is dropped:
+     <save_dir>/epoch{e}/cullavo/language_model/model.safetensors   model.layers.N.*, model.norm.weight
+     <save_dir>/epoch{e}/cullavo/vision_tower/model.safetensors     vision_model.* (trainable tower only)
    .pt files are read with torch.load(weights_only=True) only.
 """
 from __future__ import annotations
@@ -35,6 +47,10 @@ import torch
 
 VISION_PREFIX = "vision_tower."
 LM_PREFIX = "language_model."
+PEFT_PREFIX = "base_model.model."
+# arenas saved as whole-tower safetensors when trainable: arena -> (sub-directory, key prefix)
+TOWER_ARENAS = {"layers": ("language_model", LM_PREFIX), "vision": ("vision_tower", VISION_PREFIX)}
+COVERED_ARENAS = {"lora", "projector", "head", "embed", *TOWER_ARENAS}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -97,7 +113,7 @@ def _adapter_state(model, prefix: str, adapter: str) -> dict:
     out = {}
     for k, p in model.arenas["lora"].params.items():
         if k.startswith(prefix):
-            out[k[len(prefix):].replace(f".{adapter}.", ".")] = p.detach().to("cpu").contiguous()
+            out[PEFT_PREFIX + k[len(prefix):].replace(f".{adapter}.", ".")] = p.detach().to("cpu").contiguous()
     return out
 
 
@@ -117,6 +133,9 @@ def save_cullavo(model, save_dir: str, epoch: int, is_main_process: bool = True)
     from safetensors.torch import save_file
 
     from .lora import LM_TARGETS, VISION_TARGETS
+    uncovered = [n for n, a in model.arenas.items() if a.trainable and n not in COVERED_ARENAS]
+    if uncovered:
+        raise RuntimeError(f"save_cullavo: trainable arenas {uncovered} have no place in the save format")
     root = os.path.join(save_dir, f"epoch{epoch}")
     cul = os.path.join(root, "cullavo")
     os.makedirs(cul, exist_ok=True)
@@ -138,6 +157,12 @@ def save_cullavo(model, save_dir: str, epoch: int, is_main_process: bool = True)
     torch.save(sub_state("projector", "multi_modal_projector."), os.path.join(cul, "multi_modal_projector.pt"))
     torch.save(sub_state("head", "language_model.lm_head."), os.path.join(cul, "lm_head.pt"))
     torch.save(sub_state("embed", "language_model.model.embed_tokens."), os.path.join(cul, "embed_tokens.pt"))
+    for arena, (sub, prefix) in TOWER_ARENAS.items():
+        if arena in model.arenas and model.arenas[arena].trainable:
+            d = os.path.join(cul, sub)
+            os.makedirs(d, exist_ok=True)
+            save_file({k[len(prefix):]: p.detach().to("cpu").contiguous() for k, p in model.arenas[arena].params.items()},
+                      os.path.join(d, "model.safetensors"))
 
 
 def _copy_into(params: dict, state: dict, prefix: str, what: str):
@@ -168,9 +193,10 @@ def load_cullavo(model, load_dir: str):
                     for k in h.keys():
                         if "lora" not in k:
                             continue
-                        key = prefix + k
+                        rel = k[len(PEFT_PREFIX):] if k.startswith(PEFT_PREFIX) else k
+                        key = prefix + rel
                         if key not in lp:  # peft-saved keys drop the adapter name
-                            key = prefix + k.replace(".lora_A.", f".lora_A.{s.adapter}.").replace(
+                            key = prefix + rel.replace(".lora_A.", f".lora_A.{s.adapter}.").replace(
                                 ".lora_B.", f".lora_B.{s.adapter}.")
                         if key not in lp:
                             raise KeyError(f"adapter key {k} matches no LoRA parameter")  # reference: "No!"
@@ -182,6 +208,21 @@ def load_cullavo(model, load_dir: str):
                    "language_model.lm_head.", "lm_head")
         _copy_into(model.arenas["embed"].params, torch.load(os.path.join(cul, "embed_tokens.pt"), **ld),
                    "language_model.model.embed_tokens.", "embed_tokens")
+        for arena, (sub, prefix) in TOWER_ARENAS.items():
+            f = os.path.join(cul, sub, "model.safetensors")
+            if os.path.exists(f) and arena in model.arenas:
+                params = model.arenas[arena].params
+                with safe_open(f, framework="pt", device="cpu") as h, torch.no_grad():
+                    keys = set(h.keys())
+                    for k in keys:
+                        if prefix + k not in params:
+                            raise KeyError(f"{sub}/model.safetensors: unexpected key {k}")
+                        params[prefix + k].copy_(h.get_tensor(k).to(device=params[prefix + k].device,
+                                                                    dtype=params[prefix + k].dtype))
+                missing = [k for k in params if k[len(prefix):] not in keys]
+                if missing:
+                    raise KeyError(f"{sub}/model.safetensors: missing {missing[:3]}")
+                model.arenas[arena].note_written()
     rest = torch.load(load_dir, weights_only=True, map_location="cpu")
     if rest:
         model.load_state_dict({normalize_llava_key(k.split("cullavo_model.", 1)[-1]): v for k, v in rest.items()},

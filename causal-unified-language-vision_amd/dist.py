@@ -11,9 +11,16 @@ per step by the fused backward Functions, so a bucket is just a slice of that bu
    step runs at link bandwidth, small enough to start while most of the backward remains);
  * when the last parameter of a bucket has been written (arena write hook, i.e. its dW kernel
    is enqueued), an event is recorded on the compute stream, the comm stream waits on it and
-   the all-reduce (average) is issued there; compute continues on the next layer;
- * finish() launches whatever is left and makes the compute stream wait for the comm stream,
-   so the optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics.
+   the all-reduce is issued there; compute continues on the next layer;
+ * buckets are issued in ONE fixed global order (bucket i only after buckets 0..i-1), so every
+   rank pairs the same buffers in the same collective sequence even when their backward
+   passes write parameters in different orders (a rank whose batch has no image writes the
+   projector only when its unwritten gradients are zeroed at the end of the backward);
+ * finish() zero-commits what the backward did not write (arena.finalize_grads), launches
+   the remaining buckets and makes the compute stream wait for the comm stream, so the
+   optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics.
+The same asynchronous code runs on every backend: RCCL reduces with ReduceOp.AVG; gloo (the
+CPU tests) sums and the 1/N scale is applied in finish() after the waits.
 """
 from __future__ import annotations
 
@@ -26,8 +33,8 @@ from .arena import ParamArena
 class GradReducer:
     def __init__(self, arenas: list[ParamArena], order: list[list[str]] | None = None, *,
                  bucket_bytes: int = 256 << 20, group=None, use_side_stream: bool = True):
-        """arenas: trainable arenas; order: parameter keys grouped in the order backward
-        produces them (defaults to reverse offset order per arena, arenas as given)."""
+        """arenas: trainable arenas, in the order backward produces them; each arena's keys in
+        reverse offset order (decoder layer L-1 first)."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.buckets: list[dict] = []
@@ -68,6 +75,7 @@ class GradReducer:
             b["work"] = None
             b["launched"] = False
         self.launched = []
+        self._next = 0  # the next bucket in the global issue order
 
     def _on_write(self, ai):
         def hook(keys):
@@ -75,13 +83,16 @@ class GradReducer:
                 return
             for k in keys:
                 bi = self._key_bucket.get((ai, k))
-                if bi is None:
-                    continue
-                b = self.buckets[bi]
-                b["pending"].discard(k)
-                if not b["pending"] and not b["launched"]:
-                    self._launch(bi)
+                if bi is not None:
+                    self.buckets[bi]["pending"].discard(k)
+            self._issue_ready()
         return hook
+
+    def _issue_ready(self):
+        """Issue the longest ready prefix of the global bucket order."""
+        while self._next < len(self.buckets) and not self.buckets[self._next]["pending"]:
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, bi):
         b = self.buckets[bi]
@@ -99,28 +110,35 @@ class GradReducer:
         self.launched.append(bi)
 
     def _allreduce(self, view):
-        if self.avg_supported:
-            return dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        w.wait()
-        view.div_(self.world)
-        return None
+        op = dist.ReduceOp.AVG if self.avg_supported else dist.ReduceOp.SUM
+        return dist.all_reduce(view, op=op, group=self.group, async_op=True)
 
     def finish(self):
-        """Launch every bucket not yet reduced; make the current stream wait for all of them."""
+        """Zero-commit unwritten gradients, issue every bucket not yet reduced (in order) and
+        make the current stream wait for all of them (sum backends: scale by 1/N after)."""
         if not self.enabled:
             return
-        for bi, b in enumerate(self.buckets):
-            if not b["launched"]:
-                self._launch(bi)
+        for ar in self.arenas:
+            ar.finalize_grads()  # commits the keys it zeroes -> hooks issue their buckets
+            # after the exchange every rank holds a defined (averaged) gradient for every key,
+            # as under DDP: nothing is skipped by the optimizer in DP mode
+            ar.skipped = set()
+        for b in self.buckets:
+            b["pending"].clear()
+        self._issue_ready()
+        assert self._next == len(self.buckets)
+        scale = 1.0 / self.world
+
+        def _complete():
+            for b in self.buckets:
+                b["work"].wait()
+                if not self.avg_supported:
+                    self.arenas[b["arena"]].grad_flat[b["lo"]:b["hi"]].mul_(scale)
+
         if self.stream is not None:
             with torch.cuda.stream(self.stream):
-                for b in self.buckets:
-                    if b["work"] is not None:
-                        b["work"].wait()
+                _complete()
             torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
         else:
-            for b in self.buckets:
-                if b["work"] is not None:
-                    b["work"].wait()
+            _complete()
         self.reset()

@@ -82,9 +82,13 @@ def lm_infer(lm, embeds, attention_mask, position_ids, cache: KVCache | None, ma
     Returns (logits [B, Lnew, V] bf16, cache)."""
     B, Lnew, d = embeds.shape
     cfg = lm.cfg
+    if embeds.dtype != torch.bfloat16:
+        raise NotImplementedError("KV-cache decode runs on the bf16 model (the f32 mode is a parity mode)")
     if cache is None:
         cache = KVCache(cfg.num_hidden_layers, B, max_len, cfg.num_attention_heads, cfg.head_dim, embeds.device)
     if cache.length == 0:
+        if Lnew > cache.max_len:  # kv_append writes rows [0, Lnew) of every sequence's cache
+            raise ValueError(f"prompt of {Lnew} rows does not fit the KV cache ({cache.max_len} rows)")
         if attention_mask is None:
             attention_mask = torch.ones(B, Lnew, dtype=torch.long, device=embeds.device)
         am = attention_mask.to(torch.int64)

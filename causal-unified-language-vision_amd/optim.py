@@ -30,6 +30,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.flat_state = [(torch.zeros(a.numel, dtype=state_dtype, device=a.device),
                             torch.zeros(a.numel, dtype=state_dtype, device=a.device)) for a in self.arenas]
         self.step_count = 0
+        # per-key step counts (torch keeps state['step'] per parameter): a key skipped in a
+        # cycle (no gradient, arena.skipped) neither moves nor advances its bias correction
+        self.key_steps = [{k: 0 for k in a.offsets} for a in self.arenas]
         dev = self.arenas[0].device if self.arenas else torch.device("cpu")
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self._coef = torch.ones(1, dtype=torch.float32, device=dev)
@@ -52,23 +55,44 @@ class FusedAdamW(torch.optim.Optimizer):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         scale = self._coef if self._clip_pending else None
-        for a, (m, v) in zip(self.arenas, self.flat_state):
-            ops.adamw(a.flat, a.grad_flat, m, v, lr=g["lr"], beta1=b1, beta2=b2, eps=g["eps"],
-                      weight_decay=g["weight_decay"], step=self.step_count, grad_scale=scale)
+        for a, (m, v), steps in zip(self.arenas, self.flat_state, self.key_steps):
+            for lo, hi, st in self._runs(a, steps):
+                ops.adamw(a.flat[lo:hi], a.grad_flat[lo:hi], m[lo:hi], v[lo:hi], lr=g["lr"], beta1=b1, beta2=b2,
+                          eps=g["eps"], weight_decay=g["weight_decay"], step=st, grad_scale=scale)
             a.note_written()
         self._clip_pending = False
+
+    @staticmethod
+    def _runs(a, steps):
+        """Advance the per-key step counts of the keys with a gradient and return the maximal
+        contiguous element ranges (lo, hi, step) sharing one step count: one launch per arena
+        when every key has a gradient and the same history (the training step)."""
+        runs = []
+        for k, (o, n, _) in sorted(a.offsets.items(), key=lambda kv: kv[1][0]):
+            if k in a.skipped:
+                continue
+            steps[k] += 1
+            if runs and runs[-1][1] == o and runs[-1][2] == steps[k]:
+                runs[-1][1] = o + n
+            else:
+                runs.append([o, o + n, steps[k]])
+        return runs
 
     def zero_grad(self, set_to_none: bool = False):
         for a in self.arenas:
             a.zero_grad()
 
     def state_dict(self):
-        return {"step": self.step_count, "lr": self.param_groups[0]["lr"],
+        return {"step": self.step_count, "lr": self.param_groups[0]["lr"], "key_steps": [dict(s) for s in self.key_steps],
                 "exp_avg": [m for m, _ in self.flat_state], "exp_avg_sq": [v for _, v in self.flat_state]}
 
     def load_state_dict(self, sd):
         self.step_count = sd["step"]
         self.param_groups[0]["lr"] = sd["lr"]
+        if "key_steps" in sd:
+            self.key_steps = [dict(s) for s in sd["key_steps"]]
+        else:
+            self.key_steps = [{k: self.step_count for k in a.offsets} for a in self.arenas]
         for (m, v), m2, v2 in zip(self.flat_state, sd["exp_avg"], sd["exp_avg_sq"]):
             m.copy_(m2)
             v.copy_(v2)

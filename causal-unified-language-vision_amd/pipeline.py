@@ -2,7 +2,9 @@
 pipeline/CuLLaVOPipeline.py:26-133 and modeling/architectures/cullavo_model.py:12-214.
 
 The reference's forward_step1/2 first turn raw records into prompts (cullavo/arch_cullavo.py:96-339,
-397-543). forward_step2 does the same here when it is given lbk.json records and a processor
+397-543); its eval mode runs the step-2-pre generation (cullavo_model.py:53-58, :73-76 ->
+arch_cullavo.py:341-395) through CuLLaVOModel.generate on the KV cache, and evaluate_model gathers
+the new entries across ranks (CuLLaVOPipeline.py:95-133). forward_step2 does the same here when it is given lbk.json records and a processor
 (prompting.step2_process: prompt/label builder + GPU image preprocessing); step 1's
 detectron2 box drawing is out of scope, so it (like step 2 without a processor) takes the
 already-tokenised tensors the prompt builder would have produced. Both return
@@ -51,13 +53,56 @@ class CuLLaVO(nn.Module):
         return cls(cfg, m)
 
     def forward(self, batched_inputs, accel=None, mode=None):
+        """reference cullavo_model.py:45-58"""
         if self.training:
             if self.cfg["NAME"] == "cullavo_step1.yaml":
                 return self.forward_step1(batched_inputs)
             if self.cfg["NAME"] == "cullavo_step2.yaml":
                 return self.forward_step2(batched_inputs, accel)
             raise ValueError(f"unknown step config {self.cfg['NAME']}")
-        raise NotImplementedError("evaluation / step-2-pre generation needs KV-cache decode (SURVEY.md §8(f) row 2)")
+        if self.cfg["NAME"] == "cullavo_step2_pre.yaml":
+            return self.forward_step2_pre(batched_inputs, accel)
+        return self.evaluate_with_llm(batched_inputs, accel)
+
+    def _device(self, accel):
+        return accel.device if accel is not None else torch.device("cuda", torch.cuda.current_device())
+
+    def forward_step2_pre(self, batched_inputs, accel=None, **kw):
+        """reference cullavo_model.py:73-76: lbk records -> new lbk.json entries (generation)"""
+        if self.cullavo_processor is None:
+            raise ValueError("step-2-pre generation needs a CuLLaVOProcessor (tokenizer)")
+        return self.cullavo_model.step2_preprocess(batched_inputs, self.cullavo_processor, self._device(accel), **kw)
+
+    def evaluate_with_llm(self, batched_inputs, accel=None, **generate_kwargs):
+        """reference cullavo_model.py:85-149: resize the records' images to 336x336, ask for the
+        objects and their boxes, generate with the reference's sampling settings and return the
+        decoded answers (the reference's version is a debugging scratchpad that overwrites its
+        inputs seven times and draws with detectron2; its effective generation is this one,
+        per record, with the parsed boxes attached)."""
+        import torch.nn.functional as F
+
+        from .prompting import STEP2_PRE_GENERATE, box_and_class_parser
+        if self.cullavo_processor is None:
+            raise ValueError("evaluation needs a CuLLaVOProcessor (tokenizer)")
+        size = self.cullavo_model.config.vision_config.image_size
+        dev = self._device(accel)
+        gk = dict(STEP2_PRE_GENERATE, **generate_kwargs)
+        out = []
+        for x in batched_inputs:
+            img = F.interpolate(torch.as_tensor(x["image"])[None].float(), size=(size, size))[0]
+            inputs = self.cullavo_model.eval_process(
+                images=img.round().clamp(0, 255).to(torch.uint8),
+                prompt="provide multiple object names with their numbering index and the objects' bounding box "
+                       "coordinates in this image.", processor=self.cullavo_processor, device=dev)
+            with torch.inference_mode():
+                ids = self.cullavo_model.generate(**inputs, **gk)
+            text = self.cullavo_processor.batch_decode(ids, skip_special_tokens=True)[0]
+            try:
+                boxes, classes, flag = box_and_class_parser(text)
+            except Exception:
+                boxes, classes, flag = None, None, True
+            out.append({"text": text, "boxes": None if flag else boxes.tolist(), "classes": None if flag else classes})
+        return out
 
     def forward_step(self, batched_inputs):
         """forward_step1 / forward_step2 (reference :60-83) on pre-tokenised inputs"""
@@ -123,7 +168,7 @@ class CuLLaVOPipeline:
 
     def get_dataloaders(self, trainer, dataset_label: str, is_evaluation: bool):
         if is_evaluation:
-            raise NotImplementedError("evaluation loaders: SURVEY.md §8(f) rows 2 and 4")
+            return self._eval_loader(trainer, dataset_label)
         if not hasattr(self, "train_loader"):
             d = self._opt["DATA"]
             cm = trainer.model.cullavo_model
@@ -156,5 +201,52 @@ class CuLLaVOPipeline:
                 trainer.update_model()
         return loss_info, sample_size_info, {}
 
+    def _eval_loader(self, trainer, dataset_label: str):
+        """lbk records of one evaluation dataset (reference datasets/build.py test loaders over
+        register_lbkllava_datasets.py), sharded across ranks like accel.prepare: rank r takes
+        records r, r + N, ... in batches of BATCH_SIZE_PER_GPU (lists of record dicts, as the
+        reference's collate=list does). opt['DATA']['EVAL_RECORDS'][label] holds the records
+        (or a path to an lbk.json, read with prompting.load_lbk_records)."""
+        from .prompting import load_lbk_records
+        d = self._opt["DATA"]
+        src = d.get("EVAL_RECORDS", {}).get(dataset_label)
+        if src is None:
+            raise KeyError(f"no evaluation records for {dataset_label} (opt['DATA']['EVAL_RECORDS'])")
+        recs = load_lbk_records(src, d.get("IMAGE_ROOT")) if isinstance(src, str) else list(src)
+        world, rank = trainer.accel.num_processes, trainer.accel.process_index
+        mine = recs[rank::world]
+        bs = int(d.get("BATCH_SIZE_PER_GPU", 1))
+        return [mine[i:i + bs] for i in range(0, len(mine), bs)]
+
+    @staticmethod
+    def all_gather(data, world_size):
+        """reference pipeline/CuLLaVOPipeline.py:66-69"""
+        import torch.distributed as dist
+        output = [None for _ in range(world_size)]
+        dist.all_gather_object(output, data, group=None)
+        return output
+
     def evaluate_model(self, trainer):
-        raise NotImplementedError("step-2-pre generation / eval needs KV-cache decode (SURVEY.md §8(f) row 2)")
+        """reference pipeline/CuLLaVOPipeline.py:95-133: run the eval-mode model (step-2-pre
+        generation) over every TEST dataset, all_gather_object the new entries across ranks and
+        write them as one JSON list on rank 0 (opt['EVAL_OUTPUT'], default
+        <SAVE_DIR>/lbk_new_version.json). Returns the gathered list."""
+        import json
+        import os
+        model = trainer.model.eval()
+        out = []
+        with torch.no_grad():
+            for label in self._opt.get("DATASETS", {}).get("TEST", []):
+                for batch in self.get_dataloaders(trainer, label, is_evaluation=True):
+                    out.extend(model(batch, accel=trainer.accel))
+        trainer.accel.wait_for_everyone()
+        world = trainer.accel.num_processes
+        if world > 1:
+            out = [e for part in self.all_gather(out, world) for e in part]
+        if trainer.accel.is_main_process:
+            path = self._opt.get("EVAL_OUTPUT") or os.path.join(self._opt.get("SAVE_DIR", "."), "lbk_new_version.json")
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            with open(path, "w") as f:
+                json.dump(out, f)
+        trainer.accel.wait_for_everyone()
+        return out

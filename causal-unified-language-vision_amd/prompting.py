@@ -182,6 +182,80 @@ class CuLLaVOProcessor:
         pix = self.image_processor(images) if images is not None else None
         return BatchEncoding(ids, mask, pix)
 
+    def batch_decode(self, sequences, skip_special_tokens=True, **kw):
+        """LlavaProcessor.batch_decode -> the tokenizer's"""
+        return self.tokenizer.batch_decode(sequences, skip_special_tokens=skip_special_tokens, **kw)
+
+
+# ---- step-2-pre labelling (reference cullavo/arch_cullavo.py:341-395) -----------------------------
+STEP2_PRE_PROMPT = ("provide multiple object names with their numbering index and the objects' bounding box "
+                    "coordinates in the image.")
+STEP2_PRE_GENERATE = dict(do_sample=True, temperature=0.9, top_k=50, top_p=0.95, max_new_tokens=1000, use_cache=True)
+
+
+def find(s: str, ch: str) -> list[int]:
+    """reference cullavo/utils/utils.py:66-67"""
+    return [i for i, c in enumerate(s) if c == ch]
+
+
+def box_and_class_parser(decoded_text: str):
+    """reference cullavo/utils/utils.py:46-64: '(... name)' / '[x0, y0, x1, y1]' pairs of the
+    generated text -> (box tensor [n, 4], class names, flag); flag = True when the brackets do
+    not pair up. The box literal is read with ast.literal_eval instead of the reference's eval()
+    (generated text is untrusted; literal_eval accepts exactly the list literals eval() parses
+    here and raises on anything else, which the caller's except branch handles like the
+    reference's)."""
+    import ast
+    sb, eb = find(decoded_text, "["), find(decoded_text, "]")
+    sc, ec = find(decoded_text, "("), find(decoded_text, ")")
+    if len(sb) != len(eb) or len(sc) != len(ec) or len(sc) != len(sb):
+        return None, None, True
+    boxes, classes = [], []
+    for b0, b1, c0, c1 in zip(sb, eb, sc, ec):
+        boxes.append(ast.literal_eval(decoded_text[b0:b1 + 1]))
+        classes.append(decoded_text[c0 + 1:c1].split(" ")[-1])
+        if len(boxes[-1]) != 4:
+            boxes.pop(-1)
+            classes.pop(-1)
+    return torch.tensor(boxes), classes, False
+
+
+def step2_preprocess(model, batched_inputs, processor, device, *, dice=None, generate_kwargs=None, on_generate=None):
+    """reference cullavo/arch_cullavo.py:341-395: for one record in ~50 (torch.randint(0, 50) == 0)
+    generate an object/box description of its image with the reference's sampling settings
+    (T 0.9, top-k 50, top-p 0.95, 1000 new tokens, KV cache), parse boxes and classes, and emit
+    the new lbk.json entry; every other record passes through. The reference also rasterises the
+    boxes into the image with detectron2's Visualizer and saves it (:376-386): that drawing is
+    out of scope here, the entry carries the parsed boxes/classes for it. dice(record) replaces
+    the random roll, generate_kwargs override the sampling settings (tests: greedy),
+    on_generate(record, generate_ids, decoded_text) observes each generation."""
+    gk = dict(STEP2_PRE_GENERATE, **(generate_kwargs or {}))
+    new = []
+    for batch in batched_inputs:
+        if "image" not in batch:
+            new.append({"id": batch["question_id"], "conversations": batch["question"]})
+            continue
+        roll = int(torch.randint(high=50, low=0, size=(1,)).item()) if dice is None else int(dice(batch))
+        base = {"id": batch["question_id"], "image": batch.get("image_id"), "conversations": batch["question"]}
+        if roll != 0:
+            new.append(base)
+            continue
+        inputs = eval_process(images=batch["image"], prompt=STEP2_PRE_PROMPT, processor=processor, device=device,
+                              ignore_index=model.config.ignore_index)
+        with torch.inference_mode():
+            ids = model.generate(**inputs, **gk)
+        text = processor.batch_decode(ids, skip_special_tokens=True)[0]
+        if on_generate is not None:
+            on_generate(batch, ids, text)
+        try:
+            boxes, classes, flag = box_and_class_parser(text)
+            if flag:
+                continue  # the reference drops the record (:372-373)
+            new.append(dict(base, boxes=boxes.cpu().tolist(), classes=classes))
+        except Exception:  # the reference's bare except (:387-388)
+            new.append(base)
+    return new
+
 
 def _outputs(input_ids, pixel_values, attention_mask, labels=None):
     out = dict.fromkeys(["input_ids", "pixel_values", "attention_mask", "position_ids", "past_key_values",

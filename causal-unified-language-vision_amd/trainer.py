@@ -141,6 +141,19 @@ class DefaultTrainer:
             dist.broadcast(ar.flat, src=0)
             ar.note_written()
 
+    def eval(self):
+        """reference trainer/default_trainer.py:51-71: build the model, optionally load a CuLLaVO
+        checkpoint (opt['WEIGHT'] + opt['RESUME_FROM'] = .../epochN/CuLLaVO.pt) and run the
+        pipeline's evaluate_model (step-2-pre generation, gathered across ranks)."""
+        self.mode = "eval"
+        self.model = self.pipeline.initialize_model()
+        if self.opt.get("WEIGHT") and os.path.isfile(self.opt.get("RESUME_FROM", "")):
+            self.model.from_pretrained(self.opt["RESUME_FROM"], self.accel)
+        proc = self.opt.get("PROCESSOR")
+        if proc is not None:
+            self.model.model.cullavo_processor = proc
+        return self.pipeline.evaluate_model(self)
+
     def train(self):
         self.init_train()
         n_ep = int(self.opt["OPTIMIZER"]["EPOCH"])

@@ -96,7 +96,9 @@ def test_cullavo_save_format_roundtrip(tmp_path):
     from safetensors import safe_open
     with safe_open(str(root / "cullavo/language_model/adapter_model.safetensors"), "pt") as h:
         keys = list(h.keys())
-    assert "model.layers.0.self_attn.q_proj.lora_A.weight" in keys  # peft: tower-relative, no adapter name
+    # transformers save_pretrained of a PEFT-adapted tower: base_model.model. + tower-relative key,
+    # adapter name dropped (tf:modeling_utils.py:3410-3422, tf:integrations/peft.py:537-564)
+    assert "base_model.model.model.layers.0.self_attn.q_proj.lora_A.weight" in keys
     assert torch.load(root / "cullavo/lm_head.pt", weights_only=True).keys() == {"weight"}
     cfg = json.load(open(root / "cullavo/vision_tower/adapter_config.json"))
     assert (cfg["r"], cfg["lora_alpha"], cfg["layers_to_transform"]) == (64, 16.0, [1, 2])
@@ -108,3 +110,22 @@ def test_cullavo_save_format_roundtrip(tmp_path):
             assert torch.equal(dst.arenas[name].params[k], p), k
     for k, v in base_before.items():  # frozen base weights are not part of the save format
         assert torch.equal(dst.arenas["layers"].params[k], v)
+
+
+def test_full_policy_checkpoint_keeps_trained_decoder(tmp_path):
+    """'full' trains the decoder layers: save_cullavo writes them (language_model/model.safetensors)
+    and load_cullavo restores them -- nothing trained is silently dropped."""
+    src = tiny("full", seed=6)
+    with torch.no_grad():
+        src.arenas["layers"].flat.normal_(0, 0.05)
+    save_cullavo(src, str(tmp_path), epoch=1)
+    f = tmp_path / "epoch1" / "cullavo" / "language_model" / "model.safetensors"
+    assert f.exists()
+    from safetensors import safe_open
+    with safe_open(str(f), "pt") as h:
+        assert "model.layers.0.mlp.down_proj.weight" in set(h.keys())
+    dst = tiny("full", seed=7)
+    load_cullavo(dst, str(tmp_path / "epoch1" / "CuLLaVO.pt"))
+    for name in ("layers", "projector", "head", "embed"):
+        for k, p in src.arenas[name].params.items():
+            assert torch.equal(dst.arenas[name].params[k], p), k

@@ -90,12 +90,77 @@ def test_grad_reducer_gloo_world2():
         torch.testing.assert_close(torch.from_numpy(out[1][0][k]), mean)
     res, expect, launched, nb = out[0]
     assert nb >= 3
-    # buckets are launched during the backward, before all gradients were written
+    # buckets are launched during the backward, before all gradients were written, in the
+    # fixed global order
     assert launched and launched[0][1] < len(expect)
-    assert sorted(b for b, _ in launched) == list(range(nb))
+    assert [b for b, _ in launched] == list(range(nb))
 
 
-def _dp_worker(rank, world, port, q):
+def _ragged_worker(rank, world, port, q):
+    """Rank 0 writes every key in backward order; rank 1 writes them in another order and never
+    writes 'proj.w' (a rank whose batch has no image: the projector gets no gradient)."""
+    import sys
+    sys.path.insert(0, REPO)
+    try:
+        _init(rank, world, port)
+        from cullavo_amd.arena import ParamArena
+        from cullavo_amd.dist import GradReducer
+        specs = [(f"layers.{i}.w", (16, 8)) for i in range(4)] + [("proj.w", (8, 8))]
+        ar = ParamArena("layers", specs, device="cpu", dtype=torch.float32, trainable=True)
+        red = GradReducer([ar], bucket_bytes=16 * 8 * 4)  # one key per bucket
+        issued = []
+        orig = red._launch
+
+        def spy(bi):
+            issued.append(bi)
+            orig(bi)
+        red._launch = spy
+        g = torch.Generator().manual_seed(7 + rank)
+        order = ["proj.w"] + [f"layers.{i}.w" for i in reversed(range(4))]
+        if rank == 1:
+            order = ["layers.0.w", "layers.2.w", "layers.3.w", "layers.1.w"]
+        vals = {}
+        for key in order:
+            slot, _ = ar.grad_slot(key)
+            vals[key] = torch.randn(slot.shape, generator=g)
+            slot.copy_(vals[key])
+            ar.commit([key])
+        red.finish()
+        res = {k: ar.params[k].grad.clone().numpy() for k in ar.offsets}
+        q.put((rank, res, {k: v.numpy() for k, v in vals.items()}, issued, sorted(ar.skipped)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def test_grad_reducer_ragged_ranks_gloo_world2():
+    """Ranks that write their gradients in different orders, one of them missing a parameter:
+    the same buckets are reduced in the same global order (no mismatched collectives), the
+    missing gradient contributes zeros, and every rank ends with the mean."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        rank, res, vals, issued, skipped = q.get(timeout=120)
+        assert vals is not None, res
+        out[rank] = (res, vals, issued, skipped)
+    for p in ps:
+        p.join(timeout=60)
+    import numpy as np
+    for k in out[0][0]:
+        mean = (out[0][1].get(k, 0) + out[1][1].get(k, np.zeros_like(out[0][1][k]))) / 2
+        for r in range(2):
+            np.testing.assert_allclose(out[r][0][k], mean, rtol=1e-6, atol=1e-7)
+    assert out[0][2] == out[1][2] == list(range(len(out[0][2]))) and len(out[0][2]) >= 4
+    assert out[0][3] == out[1][3] == []  # DP: every key steps on the averaged gradient
+
+
+def _dp_worker(rank, world, port, q, text_only_rank=-1):
     import sys
     sys.path.insert(0, REPO)
     try:
@@ -108,6 +173,11 @@ def _dp_worker(rank, world, port, q):
         cfg_o = O.config_small_gpu()
         W = O.make_weights(cfg_o, 5)
         batches = [O.make_inputs(cfg_o, 2, 40, 4, 50 + r) for r in range(world)]
+        if text_only_rank >= 0:  # that rank's batch has no image: no pixel_values, no <image> id
+            ids, mask, _, labels = batches[text_only_rank]
+            ids = ids.clone()
+            ids[ids == cfg_o.image_token_index] = 7
+            batches[text_only_rank] = (ids, mask, None, labels[:, -ids.shape[1]:].clone())
 
         def model():
             m = CuLLaVOModel(tiny_gpu(), device="cuda", trainable="full", init="none")
@@ -115,7 +185,7 @@ def _dp_worker(rank, world, port, q):
             return m
 
         def run(m, b):
-            ids, mask, pix, labels = (t.cuda() for t in b)
+            ids, mask, pix, labels = (t.cuda() if t is not None else None for t in b)
             m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels).loss.backward()
 
         m = model()
@@ -132,6 +202,7 @@ def _dp_worker(rank, world, port, q):
                 m2 = model()
                 run(m2, b)
                 for a in m2.arenas.values():
+                    a.finalize_grads()  # a parameter the batch did not reach has a zero gradient
                     if a.trainable:
                         acc[a.name] = acc.get(a.name, 0) + a.grad_flat.float().cpu() / world
             ref = {k: v.numpy() for k, v in acc.items()}
@@ -143,11 +214,15 @@ def _dp_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_dp_step_equals_mean_of_single_gpu_grads():
+@pytest.mark.parametrize("text_only_rank", [-1, 1], ids=["both_images", "rank1_text_only"])
+def test_dp_step_equals_mean_of_single_gpu_grads(text_only_rank):
+    """Both ranks run the production reducer code (async all-reduce on the side stream, fixed
+    bucket order); with rank 1 holding a text-only batch its projector buckets are issued from
+    finish() while rank 0 issues them from the backward hooks, and the result is still the mean."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, text_only_rank)) for r in range(2)]
     for p in ps:
         p.start()
     out = {}
