@@ -38,7 +38,87 @@ def parse():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--workload", default="step", choices=["step", "vit"],
+                    help="step: the training step (default; configs 3/4/5 by --config/--batch/--text-len); "
+                         "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64)")
     return ap.parse_args()
+
+
+
+
+def vit_main(args):
+    """BASELINE config 2: CLIP ViT-L/14-336 encoder, bs 64 per GPU, forward of the 23 layers
+    hidden_states[-2] needs (what the CuLLaVO step runs; reference cullavo/arch_cullavo.py:586-597),
+    bf16, random-init weights, synthetic pixels resident in HBM. value = images/s (all ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    from cullavo_amd import ops
+    from cullavo_amd.arena import ParamArena
+    from cullavo_amd.config import CLIPVisionConfig, CuLLaVOConfig
+    from cullavo_amd.modeling import CLIPVisionTransformer, clip_specs, init_random_
+    from cullavo_amd.perf import flops_per_sample, needed_vision_layers
+    from cullavo_amd.trainer import init_distributed
+
+    init_distributed()
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    vc = CLIPVisionConfig()
+    cfg = CuLLaVOConfig(vision_config=vc)
+    ar = ParamArena("vision", clip_specs(vc, "vision_tower.vision_model."), device="cuda")
+    init_random_({"vision": ar}, seed=0)
+    vt = CLIPVisionTransformer(vc, ar.params, "vision_tower.vision_model.", ar)
+    n_layers = needed_vision_layers(cfg)
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    pix = torch.randn(args.batch, 3, vc.image_size, vc.image_size, device="cuda", generator=g)
+    fl_img = flops_per_sample(cfg, 513)["vit"]
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            vt.hidden_state(pix, n_layers)
+        torch.cuda.synchronize()
+        ops.trace_gemm("all")
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            vt.hidden_state(pix, n_layers)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    fams = gemm_families(ops.trace_launches())
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    imgs = world * args.batch * args.steps
+    tf = fl_img * args.batch / (elapsed / args.steps) / 1e12
+    top = fams[0]
+    if rank == 0:
+        line = {
+            "metric": "CLIP ViT-L/14-336 encoder images/sec (forward, hidden_states[-2])",
+            "value": round(imgs / elapsed, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded pixels in HBM, random-init weights)",
+            "config": {"workload": f"config 2: CLIP ViT-L/14-336 encoder, bs={args.batch}/GPU, 336 px, "
+                                   f"{n_layers} layers (hidden_states[-2]) + patch embed, bf16, forward",
+                       "model": "clip-vit-large-patch14-336", "global_batch": world * args.batch, "seq_len": 577,
+                       "parallelism": f"dp{world}"},
+            "model_tflops_per_gpu": round(tf, 2), "gflop_per_image": round(fl_img / 1e9, 1),
+            "roofline": {"kernel": f"whole encoder (dominant kernel {top['kernel']}, {top['role']}: "
+                                   f"{100 * top['ms'] / (elapsed * 1e3):.1f} % of the time at "
+                                   f"{top['achieved_tflops']:.0f} TFLOP/s)",
+                         "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None},
+            "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share": round(f["ms"] / (elapsed * 1e3), 4),
+                              "achieved_tflops": round(f["achieved_tflops"], 1)} for f in fams[:4]],
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(cfg, text_len: int, budget_s: float):
@@ -122,32 +202,64 @@ def cpu_baseline(cfg, text_len: int, budget_s: float):
                        f"ViT layers; {time.perf_counter() - t_start:.1f}s of CPU work")}
 
 
-def gemm_kernel_name(M, N, K):
-    """rocprof name + workgroup count of the kernel cullavo_gemm picks for a (0,0) problem"""
+def gemm_kernel_name(M, N, K, al=0, bl=0):
+    """rocprof name (template arguments as rocprofv3 prints them) + workgroup count of the
+    kernel cullavo_gemm picks for a bf16-output problem (cullavo_gemm_plan)"""
     import ctypes
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
-    tile = _lib.lib().cullavo_gemm_plan(M, N, K, 0, 0, ctypes.byref(g))
-    names = {0: "gemm_k<0, 0, 1>", 1: "gemm256_k<0, 0, 1, 256, 128>", 2: "gemm256_k<0, 0, 1, 256, 256, 1>",
-             3: "gemm256_k<0, 0, 1, 192, 256, 1>"}
-    return names[tile], int(g.value)
+    tile = _lib.lib().cullavo_gemm_plan(M, N, K, al, bl, ctypes.byref(g))
+    ldr = 1 if al == 0 else 0  # gemm.hip default_ldr
+    names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0>",
+             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>"}
+    return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 
-def measured_traffic(kname, grid):
-    """HBM bytes per launch of the roofline kernel from the committed PMC pass (None if the
-    profile was taken on a different kernel shape)."""
+GEMM_ROLE = {(0, 0): "forward Y = X W^T", (0, 1): "input gradient dX = dY W", (1, 1): "weight gradient dW = dY^T X",
+             (1, 0): "transposed-A"}
+
+
+def gemm_families(launches):
+    """Group traced GEMM launches by kernel instantiation: launches, FLOPs, ms, algorithmic HBM
+    bytes (A + B read once, C written; + C read when accumulating is not traced: beta = 0 in the
+    step) -> achieved TFLOP/s per kernel, sorted by GPU time."""
+    fam = {}
+    for (M, N, K, al, bl), ms in launches:
+        name, _ = gemm_kernel_name(M, N, K, al, bl)
+        f = fam.setdefault(name, {"kernel": name, "role": GEMM_ROLE[(al, bl)], "launches": 0, "ms": 0.0,
+                                  "flops": 0.0, "bytes": 0.0, "shapes": set()})
+        f["launches"] += 1
+        f["ms"] += ms
+        f["flops"] += 2.0 * M * N * K
+        f["bytes"] += 2.0 * (M * K + N * K + M * N)
+        f["shapes"].add((M, N, K))
+    out = sorted(fam.values(), key=lambda f: -f["ms"])
+    for f in out:
+        f["achieved_tflops"] = f["flops"] / (f["ms"] * 1e-3) / 1e12
+        f["shapes"] = sorted(f["shapes"])
+    return out
+
+
+def measured_traffic(kname):
+    """HBM bytes per launch of the roofline kernel (average over its launches in one profiled
+    step) and its MFMA busy fraction, from the committed PMC passes (None if the profile was
+    taken on another kernel)."""
     path = os.path.join(REPO, "profiles", "roofline_traffic.json")
     try:
         rec = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    if rec.get("kernel") == kname and int(rec.get("grid", -1)) == grid:
-        return rec.get("bytes_per_launch")
-    return None
+        return None, None
+    if rec.get("kernel") == kname:
+        return rec.get("bytes_per_launch"), rec.get("mfma_busy_frac")
+    return None, None
 
 
 def main():
     args = parse()
+    if args.workload == "vit":
+        if args.batch == 8:
+            args.batch = 64  # BASELINE config 2
+        return vit_main(args)
     import torch
     import torch.distributed as dist
 
@@ -176,12 +288,11 @@ def main():
         loss = step()
     torch.cuda.synchronize()
 
-    # dominant kernel: the fused gate|up GEMM of the decoder layers, timed with HIP events on
-    # the stream it is launched on
+    # every GEMM launch of the timed steps is bracketed by HIP events on the stream it runs on;
+    # the roofline object reports the kernel with the largest share of GPU time
     cfg = cm.config
     T = args.batch * (args.text_len + cfg.vision_config.num_patches - 1)
-    d, F_ = cfg.text_config.hidden_size, cfg.text_config.intermediate_size
-    ops.trace_gemm((T, 2 * F_, d, 0, 0))
+    ops.trace_gemm("all")
 
     if world > 1:
         dist.barrier()
@@ -193,7 +304,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms, kern_n = ops.trace_result()
+    fams = gemm_families(ops.trace_launches())
     if world > 1:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -206,13 +317,15 @@ def main():
     samples = world * args.batch * args.steps
     value = samples / elapsed
     step_tflops = fl["train"] * world * args.batch / (elapsed / args.steps) / 1e12
-    gemm_flops = 2.0 * T * 2 * F_ * d
-    kname, grid = gemm_kernel_name(T, 2 * F_, d)
-    traffic = measured_traffic(kname, grid)
-    achieved = gemm_flops / (kern_ms * 1e-3) / 1e12 if kern_n else None
+    top = fams[0]
+    kname = top["kernel"]
+    traffic, mfma_busy = measured_traffic(kname)
+    achieved = top["achieved_tflops"]
+    n_launch = top["launches"]
     if rank == 0:
         line = {
-            "metric": "train-step samples/sec (336px img + 512-tok prompt, 7B LM)",
+            "metric": "train-step samples/sec (336px img + 512-tok prompt, 7B LM)" if "13b" not in args.config
+                      else "train-step samples/sec (336px img + 1024-tok prompt, 13B LM)",
             "value": round(value, 4),
             "unit": "samples/s",
             "n_gpus": world,
@@ -224,7 +337,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (seeded ids/pixels/labels in HBM, random-init weights)",
-            "config": {"workload": f"config 3: ViT-L/14-336 + Vicuna-7B, seq 576+512 (L={args.text_len + 575}), "
+            "config": {"workload": f"{'config 5: ViT-L/14-336 + Llama-2-13B' if '13b' in args.config else 'config 3: ViT-L/14-336 + Vicuna-7B'}, "
+                                   f"seq 576+{args.text_len - 1} (L={args.text_len + 575}), "
                                    f"bs={args.batch}/GPU, bf16, {args.trainable} fine-tune "
                                    f"({'LoRA r=64 on the LM + ViT layers 12-22' if args.trainable == 'lora' else 'vision frozen'}), AdamW",
                        "model": args.config, "global_batch": world * args.batch,
@@ -234,19 +348,26 @@ def main():
             "mfu": round(step_tflops / world / PEAK_BF16_TFLOPS, 4),
             "loss": round(loss_v, 5),
             "roofline": {
-                "kernel": f"{kname} grid={grid}: fused gate|up projection M={T} N={2 * F_} K={d}",
+                "kernel": f"{kname}: {top['role']}, {len(top['shapes'])} shapes "
+                          f"{['x'.join(map(str, sh)) for sh in top['shapes']]} (M x N x K), "
+                          f"{n_launch // args.steps} launches/step, {100 * top['ms'] / (elapsed * 1e3):.1f} % of the step",
                 "bound": "mfma",
-                "achieved": round(achieved, 2) if achieved else None,
+                "achieved": round(achieved, 2),
                 "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4) if achieved else None,
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "bytes/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; "
-                                "profiles/roofline_traffic.json)" if traffic else None,
-                "avg_ms": round(kern_ms, 4) if kern_n else None,
-                "launches_timed": kern_n,
-                "flops_per_launch": gemm_flops,
+                "traffic_unit": "bytes/launch averaged over the kernel's launches in one step (HBM, rocprofv3 "
+                                "FETCH_SIZE x2 + WRITE_SIZE; profiles/roofline_traffic.json)" if traffic else None,
+                "algorithmic_bytes": round(top["bytes"] / n_launch),
+                "mfma_busy": mfma_busy,
+                "avg_ms": round(top["ms"] / n_launch, 4),
+                "launches_timed": n_launch,
+                "flops_per_launch": top["flops"] / n_launch,
             },
+            "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share_of_step": round(f["ms"] / (elapsed * 1e3), 4),
+                              "achieved_tflops": round(f["achieved_tflops"], 1),
+                              "frac": round(f["achieved_tflops"] / PEAK_BF16_TFLOPS, 4)} for f in fams[:6]],
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)

@@ -136,8 +136,15 @@ DEV frag8 read_frag(const char* lds, int rbase, int ks, int lane) {
 }
 
 DEV float act_apply(int act, float x) {
-  if (act == CULLAVO_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
-  if (act == CULLAVO_ACT_QUICK_GELU) return x / (1.f + __expf(-1.702f * x));
+  if (act == CULLAVO_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));  // one op: one rounding
+  if (act == CULLAVO_ACT_QUICK_GELU) {
+    // CLIP quick_gelu x * sigmoid(1.702 x) (tf:activations.py:117-123) as the reference's bf16
+    // tensors evaluate it: the product 1.702 x and the sigmoid each round to bf16, the final
+    // product rounds in the store
+    const float t = round_bf(1.702f * x);
+    const float sg = round_bf(1.f / (1.f + __expf(-t)));
+    return sg * x;
+  }
   return x;
 }
 
@@ -647,6 +654,176 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
 }
 
 // ============================================================================================
+// 256x256 tile, BK = 32, 4 LDS stages: LDS-DMA kept two K-tiles ahead across raw barriers
+// ============================================================================================
+// The 2-stage kernel above drains vmcnt(0) + a full barrier every K-tile, so each tile's DMA
+// has one tile of MFMAs (~1,000 cycles per SIMD) to land: L2 misses are exposed
+// (cdna_hip_programming.md "Pipelining across barriers": 3-buffer span beats 2-buffer overlap
+// at ~1 block/CU). Here a stage is a 32-deep K-tile (A 16 KiB + B 16 KiB), four stages fill
+// 128 KiB, tile kt+3 is issued while tile kt is computed, and the wait before each raw
+// s_barrier only retires tile kt+1 (vmcnt(8): tiles kt+2, kt+3 stay in flight).
+//   RAW: tile kt+1 is waited for before the barrier that ends iteration kt and read after it.
+//   WAR: slot (kt+3)%4 held tile kt-1, whose fragments were all read (and consumed by MFMAs)
+//        before the barrier that ended iteration kt-1, which precedes this issue.
+// Layout-0 images are [rows][32 k] with 64-B rows: 16-B chunk c of row r sits at slot
+// c ^ ((r >> 2) & 2), which makes every ds_read_b128 lane group of 16 hit 16 distinct bank slots
+// (rows r..r+15 of one fragment, chunks 0/1 or 2/3 per group). Layout-1 images are [32 k][rows]
+// read with ds_read_b64_tr_b16, as in the 64-deep kernels.
+constexpr int BK32 = 32;
+
+DEV int img0h_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 2)) << 4); }
+
+// one [ROWS][32] (layout 0) or [32][ROWS] (layout 1) operand image, 8 waves
+template <int LAYOUT, int ROWS>
+DEV void dma_tile32(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
+                    char* lds, int wave, int lane) {
+  constexpr int kPieces = ROWS / 16;  // 1 KiB pieces: 16 rows of 64 B, or 2 k-rows of ROWS*2 B (ROWS = 256)
+#pragma unroll
+  for (int i = 0; i < kPieces / 8; ++i) {
+    const int pc = wave + 8 * i;
+    unsigned off;
+    if (LAYOUT == 0) {
+      const int row = pc * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((row >> 2) & 2);
+      const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
+      off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
+    } else {
+      constexpr int RB = ROWS * 2;
+      const int byte = pc * 1024 + lane * 16;
+      const int k = byte / RB, b = byte % RB;
+      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+      const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
+      off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
+  }
+}
+
+// retire all but n (wave-uniform, in K-tiles of 4 DMA instructions) of this wave's tiles
+DEV void wait_tiles4(int n) {
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int AL, int BL, int CT>
+__global__ __launch_bounds__(512, 1) void gemm4s_k(GemmArgs p) {
+  constexpr int BM2 = 256, BN2 = 256, NST = 4;
+  constexpr int TILE_A = BM2 * BK32 * 2, TILE_B = BN2 * BK32 * 2, STAGE = TILE_A + TILE_B;
+  constexpr int TN = 4, TMW = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * p.tiles_n;
+  const int group = lid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  const int64_t m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
+  const int64_t n0 = (int64_t)((lid % per_group) / gsize) * BN2;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  f32x4 acc[TMW][TN];
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)cdiv(p.K, BK32);
+  auto stage = [&](int t) {
+    char* dst = smem + (t % NST) * STAGE;
+    const int64_t k0 = (int64_t)t * BK32;
+    dma_tile32<AL, BM2>(ra, p.lda, m0, p.M, k0, p.K, dst, wave, lane);
+    dma_tile32<BL, BN2>(rb, p.ldb, n0, p.N, k0, p.K, dst + TILE_A, wave, lane);
+  };
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nk) stage(t);
+  wait_tiles4(min(NST - 2, nk - 1));  // tile 0 landed
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt % NST) * STAGE;
+    if (kt + NST - 1 < nk) stage(kt + NST - 1);
+    frag8 fb[TN];
+    s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
+    if constexpr (BL == 1) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) tr_issue<BN2>(cur + TILE_A, wn * 64 + t * 16, 0, lane, blo[t], bhi[t]);
+    }
+    if constexpr (AL == 1) {
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * 128 + tm * 16, 0, lane, alo[tm], ahi[tm]);
+    }
+    if constexpr (BL == 1) tie_all<TN>(blo, bhi);
+    if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
+    if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      if constexpr (BL == 1) {
+        fb[t] = tr_join(blo[t], bhi[t]);
+      } else {
+        const int row = wn * 64 + t * 16 + (lane & 15);
+        fb[t] = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + TILE_A + img0h_off(row, lane >> 4)));
+      }
+    }
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm) {
+      frag8 fa;
+      if constexpr (AL == 1) {
+        fa = tr_join(alo[tm], ahi[tm]);
+      } else {
+        const int row = wm * 128 + tm * 16 + (lane & 15);
+        fa = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + img0h_off(row, lane >> 4)));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
+    }
+    // tile kt+1 must have landed before the barrier (tiles up to kt+3 may have been issued)
+    wait_tiles4(min(kt + NST - 1, nk - 1) - (kt + 1));
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  if (p.epi_lds) {
+    lds_epilogue<CT, BM2, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
+    return;
+  }
+#pragma unroll
+  for (int tm = 0; tm < TMW; ++tm) {
+    const int64_t m = m0 + wm * 128 + tm * 16 + (lane & 15);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * 64 + tn * 16 + (lane >> 4) * 4);
+  }
+}
+
+template <int AL, int BL, int CT>
+int launch4s(GemmArgs p, hipStream_t s) {
+  const int smem = 4 * (256 + 256) * BK32 * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm4s_k<AL, BL, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_n = (int)cdiv(p.N, 256);
+  gemm4s_k<AL, BL, CT><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemm4s");
+}
+
+// ============================================================================================
 // 256x256 ping-pong kernel: 8 phases per 2 K-tiles, LDS-DMA kept in flight across barriers
 // ============================================================================================
 // LDS (128 KiB): 2 buffers x 4 half-tiles of [128 local rows][64 k] (or [64 k][128]):
@@ -997,7 +1174,7 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
 // and the box-to-box spread (~10 %) is larger than their forward gain. With the steady DMA
 // removed the same schedule reaches hipBLASLt's rate (gate|up 1483 vs 1382 TF/s), so the
 // remaining loss is LDS-DMA issue cost inside the load segment (profiles/r01/gemm_8phase.md).
-enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5 };
+enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8 };
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
@@ -1026,7 +1203,7 @@ static int g_epi_lds = 1;
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = (mode >= 0 && mode <= 7) ? mode : -1;
+  g_force_tile = (mode >= 0 && mode <= 8) ? mode : -1;
   return prev;
 }
 
@@ -1041,8 +1218,8 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
   if (tile == 7 && a_layout != 0) tile = 6;
-  static const int bm[8] = {128, 256, 256, 192, 256, 256, 256, 192};
-  static const int bn[8] = {128, 128, 256, 256, 256, 256, 256, 256};
+  static const int bm[9] = {128, 256, 256, 192, 256, 256, 256, 192, 256};
+  static const int bn[9] = {128, 128, 256, 256, 256, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -1125,6 +1302,14 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     if (a_layout == 1 && b_layout == 0) { L8P(1, 0) }
     L8P(1, 1)
 #undef L8P
+  }
+  if (tile == kT4s) {
+#define L4S(AL, BL) return f32 ? launch4s<AL, BL, CULLAVO_DT_F32>(p, s) : launch4s<AL, BL, CULLAVO_DT_BF16>(p, s);
+    if (a_layout == 0 && b_layout == 0) { L4S(0, 0) }
+    if (a_layout == 0 && b_layout == 1) { L4S(0, 1) }
+    if (a_layout == 1 && b_layout == 0) { L4S(1, 0) }
+    L4S(1, 1)
+#undef L4S
   }
   if (tile >= 6) {
     if (a_layout == 0 && b_layout == 0) return launch_alt_ldr<0, 0>(p, tile, f32, s);

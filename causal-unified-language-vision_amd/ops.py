@@ -58,10 +58,16 @@ _TRACE = {"key": None, "events": []}
 
 
 def trace_gemm(key):
-    """Time every launch whose (M, N, K, a_layout, b_layout) == key with HIP events recorded on
-    the stream the kernel is launched on (bench.py's roofline); key=None stops tracing."""
+    """Time GEMM launches with HIP events recorded on the stream each kernel is launched on
+    (bench.py's roofline): key = (M, N, K, a_layout, b_layout) traces that problem, key = "all"
+    every bf16 GEMM launch; None stops tracing."""
     _TRACE["key"] = key
     _TRACE["events"] = []
+
+
+def _traced(key):
+    k = _TRACE["key"]
+    return k is not None and (k == "all" or k == key)
 
 
 def trace_result():
@@ -70,9 +76,19 @@ def trace_result():
     if not evs:
         return 0.0, 0
     evs[-1][1].synchronize()
-    ms = [a.elapsed_time(b) for a, b in evs]
+    ms = [a.elapsed_time(b) for a, b, _ in evs]
     _TRACE["key"] = None
     return sum(ms) / len(ms), len(ms)
+
+
+def trace_launches():
+    """[(problem key, ms)] of every traced launch; synchronises the events and stops tracing."""
+    evs = _TRACE["events"]
+    _TRACE["key"] = None
+    if not evs:
+        return []
+    evs[-1][1].synchronize()
+    return [(k, a.elapsed_time(b)) for a, b, k in evs]
 
 
 def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
@@ -82,7 +98,7 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
     if A.dtype == torch.float32:  # f32 parity mode: every operand f32 (cullavo_gemm_ex f32_operands)
         return gemm_ex(a_layout, b_layout, M, N, K, A, lda, B, ldb, C, ldc, alpha=alpha, bias=bias, act=act,
                        preact=preact, residual=residual, ldr=ldr, beta=beta, split_k=False)
-    traced = _TRACE["key"] is not None and _TRACE["key"] == (M, N, K, a_layout, b_layout)
+    traced = _traced((M, N, K, a_layout, b_layout))
     if traced:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(torch.cuda.current_stream())
@@ -90,7 +106,7 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
          _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _stream())
     if traced:
         e1.record(torch.cuda.current_stream())
-        _TRACE["events"].append((e0, e1))
+        _TRACE["events"].append((e0, e1, (M, N, K, a_layout, b_layout)))
     return C
 
 
@@ -132,14 +148,14 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
         if nbytes:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=C.device)
             d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
-    traced = _TRACE["key"] is not None and _TRACE["key"] == (M, N, K, a_layout, b_layout)
+    traced = not f32 and ws is None and not (drop_operand and drop_p > 0) and _traced((M, N, K, a_layout, b_layout))
     if traced:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(torch.cuda.current_stream())
     call("gemm_ex", ctypes.addressof(d), _stream())
     if traced:
         e1.record(torch.cuda.current_stream())
-        _TRACE["events"].append((e0, e1))
+        _TRACE["events"].append((e0, e1, (M, N, K, a_layout, b_layout)))
     return C
 
 

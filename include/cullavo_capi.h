@@ -116,7 +116,8 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
  * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel
  * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
- * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing).
+ * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
+ * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* Tuning/A-B switch: 1 (default) = the 8-wave kernels stage their epilogue through LDS and

@@ -43,8 +43,9 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, -1],
-                ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "t256alt", "t192alt", "auto"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, -1],
+                ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "t256alt", "t192alt", "t4stage",
+                     "auto"])
 def tile_mode(request):
     from cullavo_amd import _lib
     prev = _lib.lib().cullavo_gemm_set_tile(request.param)
