@@ -554,6 +554,309 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(
   }
 }
 
+// ============================================================================================
+// backward, 8-wave variants (the default): two waves per SIMD
+// ============================================================================================
+// The 4-wave kernels above keep one wave per SIMD (their K/V or Q/dO fragments plus two sets of
+// 32x32 accumulators need > 256 registers), so every LDS read, exp and wait of a wave sits in
+// front of its own MFMAs with nothing to overlap it. Here a workgroup has 8 waves over the same
+// 128 keys (dK/dV) or 128 queries (dQ): waves w and w + 4 own the same 32-row slice and split
+// the other dimension of every tile between them (query rows 0-31 / 32-63 of the 64-row query
+// tile; keys 0-31 / 32-63 of the 64-key tile), so each SIMD runs two waves whose MFMAs cover
+// each other's LDS / VALU phases. The pair's partial accumulators are added once at the end
+// through LDS (fixed order: half 0 + half 1), so results stay bitwise reproducible.
+//   dK/dV: K and V of the workgroup's 128 keys live in LDS for the whole sweep (row fragments
+//   re-read per tile instead of 64 registers), Q / dO tiles double-buffered beside them.
+//   dQ:    Q / dO fragments in registers, K / V tiles double-buffered in LDS.
+template <int ROWS, int D, int NT>
+struct StageN {
+  static constexpr int kPer = ROWS * D / 8 / NT;  // 16-byte chunks per thread
+  u16x8 r[kPer];
+  DEV void load(const u16* base, int64_t ld, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = threadIdx.x + NT * i;
+      const int row = q / (D / 8), ch = q % (D / 8);
+      r[i] = (row0 + row < nrows) ? *reinterpret_cast<const u16x8*>(base + (int64_t)(row0 + row) * ld + ch * 8)
+                                  : u16x8(0);
+    }
+  }
+  DEV void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = threadIdx.x + NT * i;
+      const int row = q / (D / 8), ch = q % (D / 8);
+      *reinterpret_cast<u16x8*>(lds + kv_off<D>(row, ch)) = r[i];
+    }
+  }
+};
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
+    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
+    const int32_t* __restrict__ kv_start) {
+  constexpr int QT = 64, KB = 128;
+  constexpr int TQ = QT * D * 2;          // bytes of a Q (or dO) tile
+  constexpr int TK = KB * D * 2;          // bytes of the K (or V) image
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int BUF = 2 * TQ + 2 * QT * 4;  // [Q | dO | lse(64) | delta(64)]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sK = smem;
+  char* sV = smem + TK;
+  char* bufs = smem + 2 * TK;
+
+  const int nkb = (Lk + KB - 1) / KB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, hb = lid / nkb;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int ksl = wave & 3, u = wave >> 2;          // 32-key slice, query half of each tile
+  const int key = kb * KB + ksl * 32 + (lane & 31);  // this lane's key
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
+  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
+
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dk[i] = f32x16(0.f); dv[i] = f32x16(0.f); }
+  const float c = scale * kLog2e;
+  const int kmin = kb * KB;
+  const int qt0 = CAUSAL ? (kmin / QT) : 0;
+  const int nqt = (Lq + QT - 1) / QT;
+  const bool block_live = kmin < Lk && (kmin + KB > kstart);
+
+  StageN<QT, D, 512> sq, sdo;
+  float aux = 0.f;
+  auto load_aux = [&](int qt) {
+    if (threadIdx.x < 2 * QT) {
+      const int qq = qt * QT + (int)threadIdx.x % QT;
+      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+    }
+  };
+  auto store_aux = [&](char* buf) {
+    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TQ))[threadIdx.x] = aux;
+  };
+  if (block_live) {
+    StageN<KB, D, 512> skv;
+    skv.load(Kb, ldk, kmin, Lk);
+    skv.store(sK);
+    skv.load(Vb, ldv, kmin, Lk);
+    skv.store(sV);
+    if (qt0 < nqt) {
+      sq.load(Qb, ldq, qt0 * QT, Lq);
+      sdo.load(dOb, lddo, qt0 * QT, Lq);
+      sq.store(bufs);
+      sdo.store(bufs + TQ);
+      load_aux(qt0);
+      store_aux(bufs);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
+  __syncthreads();
+
+  for (int qt = qt0; block_live && qt < nqt; ++qt) {
+    const int cur = (qt - qt0) & 1;
+    char* buf = bufs + cur * BUF;
+    char* nbuf = bufs + (cur ^ 1) * BUF;
+    const bool more = qt + 1 < nqt;
+    if (more) {
+      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
+      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+      load_aux(qt + 1);
+    }
+    const float* slse = (const float*)(buf + 2 * TQ);
+    const float* sdel = slse + QT;
+    // S[q][key], dP[q][key] for this wave's 32 query rows of the tile
+    f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 32 * u, s, lane), row_frag<D>(sK, 32 * ksl, s, lane), sacc, 0, 0, 0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TQ, 32 * u, s, lane), row_frag<D>(sV, 32 * ksl, s, lane), pacc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 32 * u + 8 * rr + 4 * hf);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 32 * u + 8 * rr + 4 * hf);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = rr * 4 + j;
+        const int qq = qt * QT + 32 * u + 8 * rr + 4 * hf + j;
+        float pv = fast_exp2(fmaf(sacc[r], c, -l4[j] * kLog2e));
+        if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
+        sacc[r] = pv;
+        pacc[r] = pv * (pacc[r] - d4[j]);
+      }
+    }
+    // dV += P^T dO ; dK += dS^T Q over this wave's 32 query rows
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8 pf = pack_frag(sacc, s);
+      const frag8 df = pack_frag(pacc, s);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TQ, 32 * u + 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_frag<D>(buf, 32 * u + 16 * s, dt * 32, lane), dk[dt], 0, 0, 0);
+      }
+    }
+    if (more) {
+      sq.store(nbuf);
+      sdo.store(nbuf + TQ);
+      store_aux(nbuf);
+    }
+    __syncthreads();
+  }
+
+  // pair reduction: half 1 parks its partial sums in LDS, half 0 adds them and stores
+  float* red = (float*)smem;  // [2 (dk, dv)][4 slices][ND][16][64] f32
+  auto slot = [&](int which, int dt, int r) { return red + ((((which * 4 + ksl) * ND + dt) * 16 + r) * 64 + lane); };
+  __syncthreads();
+  if (u == 1) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { *slot(0, dt, r) = dk[dt][r]; *slot(1, dt, r) = dv[dt][r]; }
+  }
+  __syncthreads();
+  if (u == 0) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kb * KB + ksl * 32 + acc_row(r, hf);
+        if (kk < Lk) {
+          const int d = dt * 32 + (lane & 31);
+          dK[((int64_t)b * Lk + kk) * lddk + (int64_t)h * D + d] = f2bf((dk[dt][r] + *slot(0, dt, r)) * scale);
+          dV[((int64_t)b * Lk + kk) * lddv + (int64_t)h * D + d] = f2bf(dv[dt][r] + *slot(1, dt, r));
+        }
+      }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq8_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dQ,
+    int64_t lddq, int H, int Lq, int Lk, float scale, const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 64;
+  constexpr int TILE = KT * D * 2;
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (Lq + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int qsl = wave & 3, u = wave >> 2;  // 32-query slice, key half of each tile
+  const int q = qb * 128 + qsl * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+
+  frag8 qf[NS], of[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const bool ok = q < Lq;
+    qf[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ldq + 16 * s + 8 * hf) : u16x8(0));
+    of[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(dOb + (int64_t)q * lddo + 16 * s + 8 * hf) : u16x8(0));
+  }
+  const float lse2 = (q < Lq) ? LSE[((int64_t)b * H + h) * Lq + q] * kLog2e : INFINITY;
+  const float del = (q < Lq) ? DELTA[((int64_t)b * H + h) * Lq + q] : 0.f;
+  const float c = scale * kLog2e;
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = f32x16(0.f);
+
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * 128 + 128);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  StageN<KT, D, 512> sk, sv;
+  if (t0 < ntiles) {
+    sk.load(Kb, ldk, t0 * KT, Lk);
+    sv.load(Vb, ldv, t0 * KT, Lk);
+    sk.store(smem);
+    sv.store(smem + TILE);
+  }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);
+  __syncthreads();
+  for (int t = t0; t < ntiles; ++t) {
+    const int cur = (t - t0) & 1;
+    char* bK = smem + 2 * cur * TILE;
+    char* bV = bK + TILE;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ldk, (t + 1) * KT, Lk);
+      sv.load(Vb, ldv, (t + 1) * KT, Lk);
+    }
+    f32x16 st = f32x16(0.f), dpt = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bK, 32 * u, s, lane), qf[s], st, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bV, 32 * u, s, lane), of[s], dpt, 0, 0, 0);
+    }
+    const int kbase = t * KT + 32 * u;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kbase + acc_row(r, hf);
+      float pv = fast_exp2(fmaf(st[r], c, -lse2));
+      if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
+      dpt[r] = pv * (dpt[r] - del);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const frag8 df = pack_frag(dpt, s);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bK, 32 * u + 16 * s, dt * 32, lane), df, dq[dt], 0, 0, 0);
+    }
+    if (more) {
+      char* nK = smem + 2 * (cur ^ 1) * TILE;
+      sk.store(nK);
+      sv.store(nK + TILE);
+    }
+    __syncthreads();
+  }
+  // pair reduction (key half 1 -> LDS -> half 0 adds and stores)
+  float* red = (float*)smem;  // [4 slices][ND][16][64] f32
+  auto slot = [&](int dt, int r) { return red + (((qsl * ND + dt) * 16 + r) * 64 + lane); };
+  if (u == 1) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) *slot(dt, r) = dq[dt][r];
+  }
+  __syncthreads();
+  if (u == 0 && q < Lq) {
+    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2bf((dq[dt][rr * 4 + j] + *slot(dt, rr * 4 + j)) * scale);
+        *reinterpret_cast<u16x4*>(dQb + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+  }
+}
+
 template <typename Kern>
 void set_smem(Kern k, int bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -595,6 +898,30 @@ int bwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
   return cullavo_check_launch("attn_bwd");
 }
 
+template <int D, bool CAUSAL>
+int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
+                int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
+                u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
+                const int32_t* ks, hipStream_t s) {
+  const int64_t rows = (int64_t)B * Lq * H;
+  attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
+  // dK/dV: K, V images (2 x 128 x D) + 2 x [Q | dO | lse | delta] tiles of 64 rows; the pair
+  // reduction reuses the front 2 x 4 x 32 x D f32 of it
+  const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
+  const int smem_b = std::max(4 * 64 * D * 2, 4 * 32 * D * 4);
+  static bool once = false;
+  if (!once) {
+    set_smem(attn_bwd_dkdv8_k<D, CAUSAL>, smem_a);
+    set_smem(attn_bwd_dq8_k<D, CAUSAL>, smem_b);
+    once = true;
+  }
+  attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks);
+  attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
+  return cullavo_check_launch("attn_bwd");
+}
+
 // backward tile shape (cullavo_attn_set_bwd_tiles): bit 0 -> 64 query rows per dK/dV
 // barrier, bit 1 -> 64 keys per dQ barrier (else 32); -1 = per head dim, from the MI355X
 // sweep in tools/attn_bench.py: D=128 causal 64/32 (730 vs 746 us), D=64 32/64 (636 vs 646 us)
@@ -604,7 +931,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
   const int prev = g_bwd_tiles;
-  if (mode >= -1 && mode <= 3) g_bwd_tiles = mode;
+  if (mode >= -1 && mode <= 4) g_bwd_tiles = mode;
   return prev;
 }
 
@@ -651,7 +978,18 @@ extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64
   const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v, *O = (const u16*)o, *dO = (const u16*)dout;
   u16 *dQ = (u16*)dq, *dK = (u16*)dk, *dV = (u16*)dv;
 #define BWD4(DD, CC, QQ, KK) bwd_launch<DD, CC, QQ, KK>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-  const int tiles = g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 1 : 2);
+  // default: D=128 (the LM) the 8-wave kernels (686 vs 744 us at B=8, L=1088, H=32 causal);
+  // D=64 (the ViT) the 4-wave kernels with 32-row dK/dV and 64-key dQ tiles (647 vs 797 us at
+  // B=64, T=577, H=16): there the 4-wave kernels already hold K/V in registers at < 256
+  // VGPRs and the 8-wave LDS re-reads cost more than the second wave hides (tools/attn_bench.py)
+  const int mode = g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 4 : 2);
+  if (mode == 4) {
+    if (D == 128) return causal ? bwd8_launch<128, true>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+                                : bwd8_launch<128, false>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s);
+    return causal ? bwd8_launch<64, true>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+                  : bwd8_launch<64, false>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s);
+  }
+  const int tiles = mode;
 #define BWD(DD, CC) (tiles == 3 ? BWD4(DD, CC, 64, 64) : tiles == 2 ? BWD4(DD, CC, 32, 64) \
                      : tiles == 1 ? BWD4(DD, CC, 64, 32) : BWD4(DD, CC, 32, 32))
   if (D == 128) return causal ? BWD(128, true) : BWD(128, false);

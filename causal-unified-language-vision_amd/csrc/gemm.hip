@@ -43,7 +43,14 @@ struct GemmArgs {
   float* part;        // split-K: f32 partials [gridDim.y][M][N] (register-staged kernel only)
   int kt_per;         // K-tiles per split
   int epi_lds;        // 8-wave kernels: LDS-staged 16-B epilogue (all pointers 16-B aligned)
+  int nt_store;       // C written with non-temporal stores (streamed past the caches)
 };
+
+template <typename V>
+DEV void st_c(const GemmArgs& p, V* dst, const V& v) {
+  if (p.nt_store) __builtin_nontemporal_store(v, dst);
+  else *dst = v;
+}
 
 // ---- LDS images -----------------------------------------------------------------------------
 // layout 0 image: [128 rows][64 k], 16 B chunk c of row r at chunk slot c ^ ((r >> 1) & 7)
@@ -202,7 +209,7 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
     u16x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-    *reinterpret_cast<u16x4*>(cp) = o;
+    st_c(p, reinterpret_cast<u16x4*>(cp), o);
   } else {
     float* cp = (float*)p.C + m * p.ldc + n;
     f32x4 o;
@@ -214,7 +221,7 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = v[j];
     }
-    *reinterpret_cast<f32x4*>(cp) = o;
+    st_c(p, reinterpret_cast<f32x4*>(cp), o);
   }
 }
 
@@ -268,7 +275,7 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-    *reinterpret_cast<u16x8*>(cp) = o;
+    st_c(p, reinterpret_cast<u16x8*>(cp), o);
   } else {
     float* cp = (float*)p.C + m * p.ldc + n;
     f32x4 o0, o1;
@@ -280,8 +287,8 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { o0[j] = v[j]; o1[j] = v[4 + j]; }
     }
-    *reinterpret_cast<f32x4*>(cp) = o0;
-    *reinterpret_cast<f32x4*>(cp + 4) = o1;
+    st_c(p, reinterpret_cast<f32x4*>(cp), o0);
+    st_c(p, reinterpret_cast<f32x4*>(cp + 4), o1);
   }
 }
 
@@ -1200,6 +1207,7 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 
 static int g_force_tile = -1;
 static int g_epi_lds = 1;
+static int g_nt_store = 0;
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
@@ -1209,8 +1217,9 @@ extern "C" int cullavo_gemm_set_tile(int mode) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = g_epi_lds;
-  g_epi_lds = lds_staged ? 1 : 0;
+  const int prev = g_epi_lds | (g_nt_store << 1);
+  g_epi_lds = lds_staged & 1;
+  g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }
 
@@ -1271,6 +1280,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     p.epi_lds = a16(d.C) && a16(d.bias) && a16(d.preact) && a16(residual) && a16(d.addend) &&
                 (d.addend == nullptr || d.ld_addend % 8 == 0) && g_epi_lds;
   }
+  p.nt_store = g_nt_store;
   {
     int per = 0;
     const int splits = splitk_plan(M, N, K, &per);

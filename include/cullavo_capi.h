@@ -120,9 +120,9 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
-/* Tuning/A-B switch: 1 (default) = the 8-wave kernels stage their epilogue through LDS and
-   store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
-   Returns the previous setting. */
+/* Tuning/A-B switch. Bit 0: 1 (default) = the 8-wave kernels stage their epilogue through LDS
+   and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
+   Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls. */
@@ -196,11 +196,12 @@ int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                      int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                      float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
-/* Tuning/A-B switch for cullavo_attn_bwd's tile shape: bit 0 = 64 query rows per dK/dV
-   barrier, bit 1 = 64 keys per dQ barrier (else 32). Results are bitwise identical across
-   modes (same products summed in the same order). -1 (the default) picks per head dim
-   (D=128: 64/32, D=64: 32/64). Out-of-range values leave the mode unchanged. Returns the
-   previous mode. */
+/* Tuning/A-B switch for cullavo_attn_bwd: 4 = the 8-wave kernels (two waves per SIMD; waves
+   w and w+4 split each tile and add their partial sums once, in a fixed order); 0-3 = the
+   4-wave kernels; -1 (the default) = 4 for D=128, 2 for D=64 (measured per head dim).
+   In 0-3 with bit 0 = 64 query rows per dK/dV barrier, bit 1 = 64
+   keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
+   in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */
 int cullavo_attn_set_bwd_tiles(int mode);
 
 /* ---- KV-cache decode (generate) --------------------------------------

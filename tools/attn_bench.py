@@ -31,11 +31,15 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
     fl = 4.0 * B * H * L * L * D * (0.5 if causal else 1.0)
     tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
     res = []
-    for mode in range(4):
+    outs = {}
+    for mode in (4, 1, 2):  # 4 = the 8-wave kernels (default), 1 / 2 = the 4-wave kernels
         _lib.lib().cullavo_attn_set_bwd_tiles(mode)
         tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
                                          causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
                                          dv=dqkv[:, 2 * H * D:]))
+        outs[mode] = dqkv.float().clone()
         res.append(f"m{mode} {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.1f} TF")
+    diff = ((outs[4] - outs[1]).norm() / outs[1].norm()).item()
+    res.append(f"rel(m4, m1) {diff:.1e}")
     _lib.lib().cullavo_attn_set_bwd_tiles(-1)
     print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd " + " | ".join(res))

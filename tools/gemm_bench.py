@@ -52,9 +52,10 @@ def main():
             tb = timeit(ref[kind], a.iters)
             line = f"{name:8s} {kind:3s} T={T} out={out_f} in={in_f}  hipBLASLt {fl / tb / 1e9:7.1f} TF"
             for mode in [m.strip() for m in a.modes.split(",")]:
-                lane_epi = mode.endswith("L")  # e.g. "-1L": same kernel, per-lane epilogue
-                lib.cullavo_gemm_set_tile(int(mode.rstrip("L")))
-                lib.cullavo_gemm_set_epilogue(0 if lane_epi else 1)
+                lane_epi = "L" in mode  # e.g. "-1L": same kernel, per-lane epilogue
+                nt = "N" in mode        # e.g. "-1N": non-temporal C stores
+                lib.cullavo_gemm_set_tile(int(mode.rstrip("LN")))
+                lib.cullavo_gemm_set_epilogue((0 if lane_epi else 1) | (2 if nt else 0))
                 o = ours[kind]()
                 err = ((o.float() - r.float()).norm() / r.float().norm()).item()
                 t = timeit(ours[kind], a.iters)
