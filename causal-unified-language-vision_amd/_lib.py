@@ -80,6 +80,11 @@ def lib():
             fn.argtypes = [_argtype(t) for t, _ in params]
             fn.restype = {"int": ctypes.c_int, "size_t": ctypes.c_size_t}.get(ret, ctypes.c_char_p)
         _lib = L
+        # tuning switches for A/B runs (tools, bench): kernel-choice overrides from the env
+        if os.environ.get("CULLAVO_ATTN_BWD_MODE"):
+            L.cullavo_attn_set_bwd_tiles(int(os.environ["CULLAVO_ATTN_BWD_MODE"]))
+        if os.environ.get("CULLAVO_GEMM_TILE"):
+            L.cullavo_gemm_set_tile(int(os.environ["CULLAVO_GEMM_TILE"]))
     return _lib
 
 

@@ -898,7 +898,9 @@ int bwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
   return cullavo_check_launch("attn_bwd");
 }
 
-template <int D, bool CAUSAL>
+// DQ8: the 8-wave dQ kernel; else the 4-wave dQ kernel with 32-key tiles (measured faster
+// in the 7B step: 251 vs 284 us per layer, the dQ sweep has half the MFMAs per tile)
+template <int D, bool CAUSAL, bool DQ8>
 int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
                 int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
                 u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
@@ -908,17 +910,22 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
   // dK/dV: K, V images (2 x 128 x D) + 2 x [Q | dO | lse | delta] tiles of 64 rows; the pair
   // reduction reuses the front 2 x 4 x 32 x D f32 of it
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
-  const int smem_b = std::max(4 * 64 * D * 2, 4 * 32 * D * 4);
+  const int smem_b = DQ8 ? std::max(4 * 64 * D * 2, 4 * 32 * D * 4) : 4 * 32 * D * 2;
   static bool once = false;
   if (!once) {
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL>, smem_a);
-    set_smem(attn_bwd_dq8_k<D, CAUSAL>, smem_b);
+    if (DQ8) set_smem(attn_bwd_dq8_k<D, CAUSAL>, smem_b);
+    else set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
     once = true;
   }
   attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
       q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks);
-  attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
+  if (DQ8)
+    attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
+  else
+    attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
@@ -931,7 +938,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
   const int prev = g_bwd_tiles;
-  if (mode >= -1 && mode <= 4) g_bwd_tiles = mode;
+  if (mode >= -1 && mode <= 5) g_bwd_tiles = mode;
   return prev;
 }
 
@@ -978,16 +985,22 @@ extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64
   const u16 *Q = (const u16*)q, *K = (const u16*)k, *V = (const u16*)v, *O = (const u16*)o, *dO = (const u16*)dout;
   u16 *dQ = (u16*)dq, *dK = (u16*)dk, *dV = (u16*)dv;
 #define BWD4(DD, CC, QQ, KK) bwd_launch<DD, CC, QQ, KK>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-  // default: D=128 (the LM) the 8-wave kernels (686 vs 744 us at B=8, L=1088, H=32 causal);
+  // default: D=128 (the LM) the 8-wave dK/dV kernel + the 4-wave 32-key dQ kernel (mode 4;
+  // in the 7B step 356 + 251 us per layer vs 467 + 251 for the 4-wave pair; the 8-wave dQ
+  // kernel, mode 5, took 284 us);
   // D=64 (the ViT) the 4-wave kernels with 32-row dK/dV and 64-key dQ tiles (647 vs 797 us at
   // B=64, T=577, H=16): there the 4-wave kernels already hold K/V in registers at < 256
   // VGPRs and the 8-wave LDS re-reads cost more than the second wave hides (tools/attn_bench.py)
   const int mode = g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 4 : 2);
-  if (mode == 4) {
-    if (D == 128) return causal ? bwd8_launch<128, true>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-                                : bwd8_launch<128, false>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s);
-    return causal ? bwd8_launch<64, true>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-                  : bwd8_launch<64, false>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s);
+  if (mode == 4 || mode == 5) {
+#define B8(DD, CC, Q8) bwd8_launch<DD, CC, Q8>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+    if (mode == 5) {
+      if (D == 128) return causal ? B8(128, true, true) : B8(128, false, true);
+      return causal ? B8(64, true, true) : B8(64, false, true);
+    }
+    if (D == 128) return causal ? B8(128, true, false) : B8(128, false, false);
+    return causal ? B8(64, true, false) : B8(64, false, false);
+#undef B8
   }
   const int tiles = mode;
 #define BWD(DD, CC) (tiles == 3 ? BWD4(DD, CC, 64, 64) : tiles == 2 ? BWD4(DD, CC, 32, 64) \

@@ -196,9 +196,10 @@ int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                      int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                      float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
-/* Tuning/A-B switch for cullavo_attn_bwd: 4 = the 8-wave kernels (two waves per SIMD; waves
-   w and w+4 split each tile and add their partial sums once, in a fixed order); 0-3 = the
-   4-wave kernels; -1 (the default) = 4 for D=128, 2 for D=64 (measured per head dim).
+/* Tuning/A-B switch for cullavo_attn_bwd: 4 = the 8-wave dK/dV kernel (two waves per SIMD;
+   waves w and w+4 split each query tile and add their partial sums once, in a fixed order)
+   with the 4-wave 32-key dQ kernel; 5 = both kernels 8-wave; 0-3 = the 4-wave kernels;
+   -1 (the default) = 4 for D=128, 2 for D=64 (measured per head dim).
    In 0-3 with bit 0 = 64 query rows per dK/dV barrier, bit 1 = 64
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
    in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */

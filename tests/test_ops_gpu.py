@@ -334,16 +334,17 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode {mode}"
     # mode 4 (8-wave kernels: the pair halves of each tile are summed once at the end) adds the
     # same products in another order: bf16-rounding-level differences only, and deterministic
-    _lib.lib().cullavo_attn_set_bwd_tiles(4)
-    try:
-        o4 = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
-        o4b = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
-    finally:
-        _lib.lib().cullavo_attn_set_bwd_tiles(prev)
-    for name, a, b, c in zip("qkv", outs[0], o4, o4b):
-        assert torch.equal(b.view(torch.int16), c.view(torch.int16)), f"d{name} mode 4 not deterministic"
-        err = ((a.float() - b.float()).norm() / a.float().norm()).item()
-        assert err <= 5e-3, (name, err)
+    for mode8 in (4, 5):
+        _lib.lib().cullavo_attn_set_bwd_tiles(mode8)
+        try:
+            o4 = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
+            o4b = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
+        finally:
+            _lib.lib().cullavo_attn_set_bwd_tiles(prev)
+        for name, a, b, c in zip("qkv", outs[0], o4, o4b):
+            assert torch.equal(b.view(torch.int16), c.view(torch.int16)), f"d{name} mode {mode8} not deterministic"
+            err = ((a.float() - b.float()).norm() / a.float().norm()).item()
+            assert err <= 5e-3, (name, mode8, err)
 
 
 def test_attention_strided_and_kv_start():

@@ -32,7 +32,7 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
     tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
     res = []
     outs = {}
-    for mode in (4, 1, 2):  # 4 = the 8-wave kernels (default), 1 / 2 = the 4-wave kernels
+    for mode in (4, 5, 1, 2):  # 4 / 5 = 8-wave dK/dV (+ 4- / 8-wave dQ), 1 / 2 = the 4-wave kernels
         _lib.lib().cullavo_attn_set_bwd_tiles(mode)
         tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
                                          causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
