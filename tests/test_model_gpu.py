@@ -193,3 +193,45 @@ def test_adamw_skips_parameters_without_gradient():
     assert set(opt.key_steps[pi].values()) == {1}
     li = [a.name for a in opt.arenas].index("layers")
     assert set(opt.key_steps[li].values()) == {2}
+
+
+def test_from_pretrained_forward_matches_oracle(tmp_path):
+    """llava-hf checkpoint directory (config.json + two safetensors shards in the nested >= 4.45
+    key layout, weights as the reference's bf16 cast) -> CuLLaVOModel.from_pretrained streams it
+    into HBM -> the forward equals the bf16-faithful oracle on the same tensors (reference
+    cullavo/load_cullavo.py:86 from_pretrained, then arch_cullavo.py:546-677)."""
+    import json
+    from safetensors.torch import save_file
+
+    from cullavo_amd.arch_cullavo import CuLLaVOModel
+    cfg = O.config_small_gpu()
+    W = O.to_bf16(O.make_weights(cfg, 4))
+    v, t = cfg.vision, cfg.text
+    hf = {"model_type": "llava", "image_token_index": cfg.image_token_index, "pad_token_id": cfg.pad_token_id,
+          "vision_feature_layer": -2, "vision_feature_select_strategy": "default", "projector_hidden_act": "gelu",
+          "vision_config": {"image_size": v.image_size, "patch_size": v.patch_size, "hidden_size": v.hidden_size,
+                            "num_hidden_layers": v.num_hidden_layers, "num_attention_heads": v.num_attention_heads,
+                            "intermediate_size": v.intermediate_size, "hidden_act": "quick_gelu"},
+          "text_config": {"hidden_size": t.hidden_size, "num_hidden_layers": t.num_hidden_layers,
+                          "num_attention_heads": t.num_attention_heads, "intermediate_size": t.intermediate_size,
+                          "vocab_size": t.vocab_size, "rms_norm_eps": t.rms_norm_eps, "rope_theta": t.rope_theta}}
+    (tmp_path / "config.json").write_text(json.dumps(hf))
+
+    def new_layout(k):  # transformers >= 4.45 nested LlavaModel names
+        if k.startswith(("vision_tower.", "multi_modal_projector.")):
+            return "model." + k
+        if k.startswith("language_model.model."):
+            return "model.language_model." + k[len("language_model.model."):]
+        return k[len("language_model."):]  # lm_head
+    keys = sorted(W)
+    for i, part in enumerate((keys[:len(keys) // 2], keys[len(keys) // 2:])):
+        save_file({new_layout(k): W[k].contiguous() for k in part}, str(tmp_path / f"model-0000{i + 1}-of-00002.safetensors"))
+    m = CuLLaVOModel.from_pretrained(str(tmp_path), device="cuda", trainable="none")
+    for k, p in m.state_dict().items():
+        assert torch.equal(p.cpu(), W[k]), k
+    ids, mask, pix, labels = O.make_inputs(cfg, 2, 40, 4, 4)
+    loss_ref, logits_ref, aux = O.forward(W, cfg, ids, pix, mask, labels)
+    with torch.no_grad():
+        out = m(input_ids=ids.cuda(), pixel_values=pix.cuda(), attention_mask=mask.cuda(), labels=labels.cuda())
+    assert rel_l2(out.logits.float().cpu(), logits_ref.float()) <= 1e-2
+    assert abs(out.loss.item() - loss_ref.item()) <= 1e-2
