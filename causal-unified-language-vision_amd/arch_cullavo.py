@@ -82,7 +82,7 @@ class CuLLaVOModel(nn.Module):
         return m
 
     # -- reference API -------------------------------------------------------------------------
-    # ---- data step (reference cullavo/arch_cullavo.py:28-94, 397-543) ----
+    # ---- data step (reference cullavo/arch_cullavo.py:28-339, 397-543) ----
     @staticmethod
     def make_system_prompt(processor, device, ignore_index):
         from .prompting import make_system_prompt
@@ -93,6 +93,11 @@ class CuLLaVOModel(nn.Module):
         from .prompting import make_and_add_prompt_and_label
         return make_and_add_prompt_and_label(cullavo_prompt, cullavo_label, prompt, answer, processor, device,
                                              ignore_index)
+
+    def step1_process(self, inputs, processor, device, fix_num=5):
+        """reference cullavo/arch_cullavo.py:96-339 (prompting.step1_process; boxes drawn on the GPU)"""
+        from .prompting import step1_process
+        return step1_process(inputs, processor, device, self.config.ignore_index, fix_num)
 
     def step2_process(self, batched_inputs, processor, device):
         from .prompting import step2_process
@@ -183,6 +188,12 @@ class CuLLaVOModel(nn.Module):
         h, hs = lm.decode(inputs_embeds.reshape(B * L, d).contiguous(), sctx, bool(output_hidden_states))  # :638
         loss = None
         if labels is not None:  # :651-665
+            if labels.shape != (B, L):  # the reference's masked / shifted indexing raises here
+                if attention_mask is not None:
+                    raise IndexError(f"The shape of the mask [{B}, {L - 1}] at index 1 does not match the shape of "
+                                     f"the indexed tensor [{labels.shape[0]}, {labels.shape[-1] - 1}] at index 1")
+                raise ValueError(f"Expected input batch_size ({B * (L - 1)}) to match target batch_size "
+                                 f"({labels.shape[0] * (labels.shape[-1] - 1)}).")
             targets = ops.shift_targets(labels, attention_mask, cfg.ignore_index)
             loss, logits = HeadLossFn.apply(h, lm, targets, cfg.ignore_index, *lm.head_params())
         else:

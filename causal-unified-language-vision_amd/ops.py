@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, DT_BF16, DT_F32, call, lib
@@ -19,7 +20,7 @@ __all__ = [
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
     "ce_reduce", "ce_bwd", "adamw", "sumsq", "clip_coef", "scale_inplace", "kv_append", "attn_decode",
-    "clip_image_preprocess",
+    "clip_image_preprocess", "visimage_geometry", "draw_boxes",
 ]
 
 _DT = {torch.bfloat16: DT_BF16, torch.float32: DT_F32}
@@ -426,6 +427,8 @@ def row_gather2(src, a, b):
 def shift_targets(labels, mask, ignore_index: int = -100):
     _dev(labels, mask)
     B, L = labels.shape
+    if mask is not None and tuple(mask.shape) != (B, L):
+        raise ValueError(f"shift_targets: labels {tuple(labels.shape)} and attention mask {tuple(mask.shape)} differ")
     tgt = torch.empty((B * L,), dtype=torch.int64, device=labels.device)
     labels = labels.contiguous().to(torch.int64)
     mask = mask.contiguous().to(torch.int64) if mask is not None else None
@@ -436,6 +439,8 @@ def shift_targets(labels, mask, ignore_index: int = -100):
 def ce_fwd(logits, targets, ignore_index: int = -100):
     _dev(logits, targets)
     rows, V = logits.shape
+    if targets.numel() != rows:
+        raise ValueError(f"ce_fwd: {targets.numel()} targets for {rows} logit rows")
     row_loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
     row_lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     call("ce_fwd", _ptr(logits), _ld(logits), _ptr(targets), rows, V, int(ignore_index), _ptr(row_loss),
@@ -506,4 +511,72 @@ def clip_image_preprocess(images, Hr, Wr, h_bounds, h_kk, h_ksize, v_bounds, v_k
     call("clip_image_preprocess", _ptr(images), B, C, H, W, sb, sc, sy, sx, Hr, Wr, _ptr(h_bounds), _ptr(h_kk),
          int(h_ksize), _ptr(v_bounds), _ptr(v_kk), int(v_ksize), top, left, crop_h, crop_w, float(rescale),
          *[float(m) for m in mean], *[float(s) for s in std], _ptr(tmp), _ptr(out), _dt(out), _stream())
+    return out
+
+
+_VISIMAGE = {}
+
+
+def visimage_geometry(H: int, W: int, device):
+    """(rows, cols) device int32 maps and transData (sx, tx, sy, ty) of a VisImage of H x W"""
+    key = (H, W, str(device))
+    if key not in _VISIMAGE:
+        rows = np.zeros(H, np.int32)
+        cols = np.zeros(W, np.int32)
+        td = np.zeros(4, np.float64)
+        rc = lib().cullavo_visimage_geometry(H, W, rows.ctypes.data, cols.ctypes.data, td.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"cullavo_visimage_geometry({H}, {W}) failed: {lib().cullavo_last_error().decode()}")
+        _VISIMAGE[key] = (torch.from_numpy(rows).to(device), torch.from_numpy(cols).to(device),
+                          tuple(float(v) for v in td))
+    return _VISIMAGE[key]
+
+
+def draw_order(boxes: np.ndarray) -> np.ndarray:
+    """overlay_instances' order: np.argsort(-areas) on the float32 boxes (largest first)"""
+    b = np.asarray(boxes, np.float32).reshape(-1, 4)
+    return np.argsort(-np.prod(b[:, 2:] - b[:, :2], axis=1))
+
+
+def draw_boxes(images, boxes, colors, font_size: float = 16.0, alpha: float = 0.5, check: bool = True):
+    """Visualizer(img).overlay_instances(boxes, assigned_colors).get_image() for a batch.
+
+    images: uint8 [B, 3, H, W] on the GPU (any strides); boxes: per image an [n_i, 4] array of
+    (x0, y0, x1, y1) pixels (float32, as the reference passes them); colors: per image n_i RGB
+    triples. Returns a new uint8 [B, 3, H, W] tensor. check=True reads the kernel's overflow
+    flag back (one small device-to-host copy) and raises if a box exceeded its capacity."""
+    _dev(images)
+    if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[1] != 3:
+        raise ValueError("images must be a uint8 [B, 3, H, W] tensor")
+    B, _, H, W = images.shape
+    if len(boxes) != B or len(colors) != B:
+        raise ValueError("one box list and one colour list per image")
+    dev = images.device
+    rows, cols, td = visimage_geometry(H, W, dev)
+    nmax = max([len(b) for b in boxes] + [0])
+    bx = np.zeros((B, max(nmax, 1), 4), np.float32)
+    cl = np.zeros((B, max(nmax, 1), 3), np.uint8)
+    nb = np.zeros(B, np.int32)
+    for i, (b, c) in enumerate(zip(boxes, colors)):
+        b = np.asarray(b, np.float32).reshape(-1, 4)
+        if not np.isfinite(b).all():
+            raise ValueError(f"image {i}: box coordinates must be finite")
+        if len(c) != len(b):
+            raise ValueError(f"image {i}: {len(b)} boxes but {len(c)} colours")
+        order = draw_order(b)
+        bx[i, :len(b)] = b[order]
+        cl[i, :len(b)] = np.asarray(c, np.uint8).reshape(-1, 3)[order]
+        nb[i] = len(b)
+    bx_d = torch.from_numpy(bx).to(dev)
+    cl_d = torch.from_numpy(cl).to(dev)
+    nb_d = torch.from_numpy(nb).to(dev)
+    ws = torch.empty(int(lib().cullavo_draw_boxes_workspace(B, max(nmax, 1))), dtype=torch.uint8, device=dev)
+    out = torch.empty((B, 3, H, W), dtype=torch.uint8, device=dev)
+    width_px = max(font_size / 4.0, 1.0) * 100.0 / 72.0
+    a8 = int(alpha * 255 + 0.5)
+    sb, sc, sy, sx = images.stride()
+    call("draw_boxes", _ptr(images), B, 3, H, W, sb, sc, sy, sx, _ptr(rows), _ptr(cols), _ptr(bx_d), _ptr(nb_d),
+         _ptr(cl_d), nmax, *td, float(width_px), a8, _ptr(ws), _ptr(out), _stream())
+    if check and int(ws[:4].view(torch.int32).item()) != 0:
+        raise RuntimeError("draw_boxes: a box outline or its cells exceeded the kernel's capacity")
     return out

@@ -4,10 +4,10 @@ pipeline/CuLLaVOPipeline.py:26-133 and modeling/architectures/cullavo_model.py:1
 The reference's forward_step1/2 first turn raw records into prompts (cullavo/arch_cullavo.py:96-339,
 397-543); its eval mode runs the step-2-pre generation (cullavo_model.py:53-58, :73-76 ->
 arch_cullavo.py:341-395) through CuLLaVOModel.generate on the KV cache, and evaluate_model gathers
-the new entries across ranks (CuLLaVOPipeline.py:95-133). forward_step2 does the same here when it is given lbk.json records and a processor
-(prompting.step2_process: prompt/label builder + GPU image preprocessing); step 1's
-detectron2 box drawing is out of scope, so it (like step 2 without a processor) takes the
-already-tokenised tensors the prompt builder would have produced. Both return
+the new entries across ranks (CuLLaVOPipeline.py:95-133). forward_step1 / forward_step2 do the
+same here when given raw records and a processor (prompting.step1_process / step2_process:
+prompt/label builders, GPU box drawing and GPU image preprocessing); without a processor they take
+the already-tokenised tensors the prompt builders would have produced. Both return
 {'loss_llm': loss} like the reference.
 """
 from __future__ import annotations
@@ -56,7 +56,7 @@ class CuLLaVO(nn.Module):
         """reference cullavo_model.py:45-58"""
         if self.training:
             if self.cfg["NAME"] == "cullavo_step1.yaml":
-                return self.forward_step1(batched_inputs)
+                return self.forward_step1(batched_inputs, accel)
             if self.cfg["NAME"] == "cullavo_step2.yaml":
                 return self.forward_step2(batched_inputs, accel)
             raise ValueError(f"unknown step config {self.cfg['NAME']}")
@@ -109,7 +109,17 @@ class CuLLaVO(nn.Module):
         out = self.cullavo_model(**batched_inputs)
         return {"loss_llm": out.loss}
 
-    forward_step1 = forward_step
+    def forward_step1(self, batched_inputs, accel=None):
+        """reference cullavo_model.py:60-71: detectron2-style records -> step1_process (boxes drawn
+        into the images) -> model -> loss; a batch without thing instances gives loss 0"""
+        if isinstance(batched_inputs, (list, tuple)):
+            if self.cullavo_processor is None:
+                raise ValueError("forward_step1 on raw records needs a CuLLaVOProcessor (tokenizer)")
+            device = self._device(accel)
+            batched_inputs = self.cullavo_model.step1_process(batched_inputs, self.cullavo_processor, device)
+            if batched_inputs["input_ids"] is None:
+                return {"loss_llm": torch.tensor([0]).to(device)}
+        return self.forward_step(batched_inputs)
 
     def forward_step2(self, batched_inputs, accel=None):
         """reference cullavo_model.py:78-83: records -> step2_process -> model -> loss"""

@@ -5,9 +5,15 @@ Drop-ins for the reference's prompt builders and the processor call they end in:
 * ``make_system_prompt`` / ``make_and_add_prompt_and_label`` — reference
   cullavo/arch_cullavo.py:28-61 (same signatures; the label of the system prompt covers the 575
   extra image slots the merge inserts).
-* ``step2_process`` / ``eval_process`` — reference :397-543 / :63-94, for conversation records.
-  Records carrying ``boxes`` need detectron2's Visualizer to draw the boxes into the image
-  (:438-452); that drawing is out of scope here and raises NotImplementedError.
+* ``step1_process`` — reference :96-339: detectron2-style instance records -> boxes drawn into
+  the image, object / colour / box question-answer prompts.
+* ``step2_process`` / ``eval_process`` — reference :397-543 / :63-94; records carrying ``boxes``
+  get them drawn into the image plus the colour / box prompts (:436-499).
+* ``overlay_boxes`` — detectron2's ``Visualizer(img).overlay_instances(boxes, assigned_colors)
+  .get_image()`` as the reference calls it (:149-153, :441-448), on the GPU
+  (csrc/boxdraw.hip: pixel-identical to matplotlib's Agg rendering of that figure).
+  Random draws (colour shuffle, dice, permutations) use Python's ``random`` and torch's global
+  generator in the reference's order, so a seeded call reproduces the reference's prompts.
 * ``CuLLaVOProcessor`` — the LlavaProcessor call ``processor(text=..., images=..., padding=True,
   return_tensors="pt")``: the caller's tokenizer (any object with HF's ``__call__`` /
   ``pad_token_id`` / ``padding_side``; the real llava tokenizer is not available offline) pads
@@ -21,6 +27,7 @@ from __future__ import annotations
 
 import json
 import os
+import random
 from dataclasses import dataclass
 
 import numpy as np
@@ -67,6 +74,92 @@ def list2string(_list) -> str:
 def box2string(box) -> str:
     """reference cullavo/utils/utils.py:77-83: '[x0, y0, x1, y1]' with 3 decimals"""
     return "[" + ", ".join(f"{round(float(x), 3):.3f}" for x in box) + "]"
+
+
+def boxes2string(boxes) -> str:
+    """reference cullavo/utils/utils.py:85-91"""
+    return "[" + ", ".join(box2string(b) for b in boxes) + "]"
+
+
+def _numbered(classes, values, fmt) -> str:
+    count = {}
+    out = []
+    for x, y in zip(classes, values):
+        count[x] = count.get(x, 0) + 1
+        out.append(fmt(count[x], x, y))
+    return ", ".join(out)
+
+
+def classescolors2string(classes, colors) -> str:
+    """reference cullavo/utils/utils.py:93-103: '(#1 person) red, (#2 person) blue'"""
+    return _numbered(classes, colors, lambda n, x, y: f"(#{n} {x}) {y}")
+
+
+def classesboxes2string(classes, boxes) -> str:
+    """reference cullavo/utils/utils.py:106-116: '(#1 person) [x0, y0, x1, y1], ...'"""
+    return _numbered(classes, boxes, lambda n, x, y: f"(#{n} {x}) {box2string(y)}")
+
+
+def classes2string(classes) -> str:
+    """reference cullavo/utils/utils.py:118-128: '(#1) person, (#2) person'"""
+    return _numbered(classes, classes, lambda n, x, y: f"(#{n}) {x}")
+
+
+# reference cullavo/utils/utils.py:14-33 and the matplotlib (CSS4) colours those names draw with
+COLOR_LIST = ["white", "red", "orange", "coral", "yellow", "green", "blue", "navy", "gold", "pink", "purple",
+              "brown", "violet", "olive", "lime", "cyan", "magenta", "silver", "gray", "black"]
+COLOR_RGB = {
+    "white": (255, 255, 255), "red": (255, 0, 0), "orange": (255, 165, 0), "coral": (255, 127, 80),
+    "yellow": (255, 255, 0), "green": (0, 128, 0), "blue": (0, 0, 255), "navy": (0, 0, 128),
+    "gold": (255, 215, 0), "pink": (255, 192, 203), "purple": (128, 0, 128), "brown": (165, 42, 42),
+    "violet": (238, 130, 238), "olive": (128, 128, 0), "lime": (0, 255, 0), "cyan": (0, 255, 255),
+    "magenta": (255, 0, 255), "silver": (192, 192, 192), "gray": (128, 128, 128), "black": (0, 0, 0),
+}
+# reference utils/constants.py:1 (COCO panoptic: 80 thing + 53 stuff classes)
+COCO_PANOPTIC_CLASSES = [
+    'person', 'bicycle', 'car', 'motorcycle', 'airplane', 'bus', 'train', 'truck', 'boat',
+    'traffic light', 'fire hydrant', 'stop sign', 'parking meter', 'bench', 'bird', 'cat', 'dog',
+    'horse', 'sheep', 'cow', 'elephant', 'bear', 'zebra', 'giraffe', 'backpack', 'umbrella', 'handbag',
+    'tie', 'suitcase', 'frisbee', 'skis', 'snowboard', 'sports ball', 'kite', 'baseball bat',
+    'baseball glove', 'skateboard', 'surfboard', 'tennis racket', 'bottle', 'wine glass', 'cup',
+    'fork', 'knife', 'spoon', 'bowl', 'banana', 'apple', 'sandwich', 'orange', 'broccoli', 'carrot',
+    'hot dog', 'pizza', 'donut', 'cake', 'chair', 'couch', 'potted plant', 'bed', 'dining table',
+    'toilet', 'tv', 'laptop', 'mouse', 'remote', 'keyboard', 'cell phone', 'microwave', 'oven',
+    'toaster', 'sink', 'refrigerator', 'book', 'clock', 'vase', 'scissors', 'teddy bear', 'hair drier',
+    'toothbrush', 'banner', 'blanket', 'bridge', 'cardboard', 'counter', 'curtain', 'door-stuff',
+    'floor-wood', 'flower', 'fruit', 'gravel', 'house', 'light', 'mirror-stuff', 'net', 'pillow',
+    'platform', 'playingfield', 'railroad', 'river', 'road', 'roof', 'sand', 'sea', 'shelf', 'snow',
+    'stairs', 'tent', 'towel', 'wall-brick', 'wall-stone', 'wall-tile', 'wall-wood', 'water-other',
+    'window-blind', 'window-other', 'tree-merged', 'fence-merged', 'ceiling-merged',
+    'sky-other-merged', 'cabinet-merged', 'table-merged', 'floor-other-merged', 'pavement-merged',
+    'mountain-merged', 'grass-merged', 'dirt-merged', 'paper-merged', 'food-other-merged',
+    'building-other-merged', 'rock-merged', 'wall-other-merged', 'rug-merged',
+]
+VISUALIZER_FONT_SIZE = 16  # vis._default_font_size = 16 (reference :150, :444)
+
+
+def overlay_boxes(images, boxes, colors, device=None):
+    """Visualizer(img); _default_font_size = 16; overlay_instances(boxes=boxes,
+    assigned_colors=colors).get_image() for each image (reference :149-153, :441-448).
+
+    images: uint8 [3, H, W] tensors (a [B, 3, H, W] batch or a list of any sizes); boxes: per
+    image an [n, 4] float32 (x0, y0, x1, y1) pixel array; colors: per image n colour names of
+    COLOR_RGB. Returns uint8 [3, H, W] tensors on ``device`` (the GPU), one per image."""
+    if isinstance(images, torch.Tensor) and images.dim() == 3:
+        images, boxes, colors = [images], [boxes], [colors]
+    imgs = list(images)
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    out = [None] * len(imgs)
+    groups = {}
+    for i, im in enumerate(imgs):
+        groups.setdefault(tuple(im.shape), []).append(i)
+    for shape, idx in groups.items():
+        batch = torch.stack([torch.as_tensor(imgs[i]) for i in idx]).to(dev)
+        res = ops.draw_boxes(batch, [np.asarray(boxes[i], np.float32).reshape(-1, 4) for i in idx],
+                             [[COLOR_RGB[c] for c in colors[i]] for i in idx], font_size=VISUALIZER_FONT_SIZE)
+        for j, i in enumerate(idx):
+            out[i] = res[j]
+    return out
 
 
 # ---- images ------------------------------------------------------------------------------------
@@ -265,11 +358,36 @@ def _outputs(input_ids, pixel_values, attention_mask, labels=None):
     return out
 
 
-def step2_process(batched_inputs, processor, device, ignore_index=-100, image_size=336):
-    """reference cullavo/arch_cullavo.py:397-543 for conversation records: per record the system
-    prompt, then each (question, answer) turn ('<image>' stripped from the first question),
-    images stacked (zeros [3, 336, 336] for text-only records), one processor call, labels
-    right-padded with ignore_index"""
+def _draw_default(image, boxes, colors):
+    """one image through overlay_boxes (GPU)"""
+    return overlay_boxes([torch.as_tensor(image)], [boxes], [colors])[0]
+
+
+def _stack(images):
+    """torch.stack on one device (the GPU when any image is there), or the list for mixed sizes"""
+    dev = next((im.device for im in images if im.is_cuda), torch.device("cpu"))
+    images = [im.to(dev) for im in images]
+    if len({tuple(im.shape) for im in images}) == 1:
+        return torch.stack(images)
+    return images
+
+
+def _finish(prompts, labels, images, processor, device, ignore_index):
+    enc = processor(text=prompts, images=_stack(images), padding=True, return_tensors="pt")
+    lab = torch.nn.utils.rnn.pad_sequence([x.cpu() for x in labels], batch_first=True, padding_value=ignore_index)
+    return _outputs(enc.input_ids.to(device), enc.pixel_values.to(device) if enc.pixel_values is not None else None,
+                    enc.attention_mask.to(device), lab.to(device))
+
+
+def step2_process(batched_inputs, processor, device, ignore_index=-100, image_size=336, draw=None):
+    """reference cullavo/arch_cullavo.py:397-543: per record the system prompt, then each
+    (question, answer) turn ('<image>' stripped from the first question); a record with
+    ``boxes`` (normalised x0 y0 x1 y1) gets them drawn into its image (x 336, colours from a
+    fresh shuffle of COLOR_LIST; the record's image is replaced like the reference's :448) and
+    the colour prompt plus up to 5 colour <-> box prompts (:450-499); images stacked (zeros
+    [3, 336, 336] for text-only records), one processor call, labels right-padded with
+    ignore_index. ``draw(image, boxes_px, colour_names)`` replaces the GPU drawing (tests)."""
+    draw = draw or _draw_default
     images, prompts, labels = [], [], []
     for batch in batched_inputs:
         p, lab = make_system_prompt(processor, device, ignore_index)
@@ -279,20 +397,124 @@ def step2_process(batched_inputs, processor, device, ignore_index=-100, image_si
             p, lab = make_and_add_prompt_and_label(p, lab, text, q[2 * k + 1]["value"], processor, device,
                                                    ignore_index)
         if "boxes" in batch:
-            raise NotImplementedError("box-drawing prompts need detectron2's Visualizer "
-                                      "(reference cullavo/arch_cullavo.py:438-452): out of scope")
+            cl = list(COLOR_LIST)
+            random.shuffle(cl)
+            bt = torch.tensor(batch["boxes"])
+            n = len(batch["boxes"])
+            batch["image"] = draw(batch["image"], (bt * 336).numpy(), cl[:n])
+            colors = cl[:n]
+            answer = (f"Sure, it is {list2string(colors)} color. There is a bounding box in the image." if n == 1
+                      else f"Sure, it is {list2string(colors)} color. There are {n} bounding boxes in the image.")
+            p, lab = make_and_add_prompt_and_label(p, lab, "provide multiple bounding box colors in the image.",
+                                                   answer, processor, device, ignore_index)
+            for r_int in torch.randperm(n)[:5]:
+                box, color = bt[r_int], cl[r_int]
+                if torch.randint(high=2, low=0, size=(1,)).item() == 0:
+                    qa = (f"provide a bounding box coordinate of {color} bounding box color.",
+                          f"Sure, it is {box2string(box)}. There is a {color} bounding box color")
+                else:
+                    qa = (f"provide a bounding box color of bounding box coordinate {box2string(box)}.",
+                          f"Sure, it is {color} color.")
+                p, lab = make_and_add_prompt_and_label(p, lab, *qa, processor, device, ignore_index)
         if "image" in batch:
             images.append(torch.as_tensor(batch["image"]))
         else:
             images.append(torch.zeros(3, image_size, image_size, dtype=torch.uint8))
         prompts.append(p)
         labels.append(lab)
-    enc = processor(text=prompts, images=torch.stack([im.cpu() for im in images]), padding=True,
-                    return_tensors="pt")
-    lab = torch.nn.utils.rnn.pad_sequence([x.cpu() for x in labels], batch_first=True,
-                                          padding_value=ignore_index)
-    return _outputs(enc.input_ids.to(device), enc.pixel_values.to(device) if enc.pixel_values is not None else None,
-                    enc.attention_mask.to(device), lab.to(device))
+    return _finish(prompts, labels, images, processor, device, ignore_index)
+
+
+def _class_name(c) -> str:
+    return COCO_PANOPTIC_CLASSES[int(c)].replace("-merged", "").replace("-other", "").replace("-stuff", "")
+
+
+def _box_tensor(gt_boxes) -> torch.Tensor:
+    return gt_boxes.tensor if hasattr(gt_boxes, "tensor") else torch.as_tensor(gt_boxes)
+
+
+def step1_process(inputs, processor, device, ignore_index=-100, fix_num=5, draw=None):
+    """reference cullavo/arch_cullavo.py:96-339 (step 1: object understanding).
+
+    inputs: detectron2-style records {"image": uint8 [3, H, W], "instances": object with
+    ``is_things``, ``gt_classes`` (COCO panoptic ids) and ``gt_boxes`` (Boxes or an [n, 4]
+    pixel tensor)}. For each record with thing instances (at most 20, one per colour): the boxes
+    drawn into the image in a shuffled colour order, then the prompts — objects with their
+    boxes, the box colours, one class -> colours / boxes question picked by a die, and up to
+    ``fix_num`` colour <-> box and box / colour -> class questions — with the reference's
+    random draws in its order (one ``random.shuffle`` per call, ``torch.randint`` /
+    ``torch.randperm`` per record). Returns the model inputs, or {"input_ids": None} when no
+    record has a thing instance (:309). The reference scales the record's Boxes in place
+    (:145); this leaves the record untouched. Its drawing multiplies both coordinates by the
+    image height (:151), reproduced as is."""
+    draw = draw or _draw_default
+    cl = list(COLOR_LIST)
+    random.shuffle(cl)
+    images, prompts, labels = [], [], []
+    for inp in inputs:
+        inst = inp["instances"]
+        things = [i for i, t in enumerate(inst.is_things) if t]
+        idx = torch.tensor(things, dtype=torch.long)[:len(cl)]
+        if len(idx) == 0:
+            continue
+        cls_ids = torch.as_tensor(inst.gt_classes)[idx]
+        names = [_class_name(c) for c in cls_ids]
+        uniq = cls_ids.unique()
+        uniq_names = [_class_name(c) for c in uniq]
+        _, H, W = inp["image"].shape
+        gt = _box_tensor(inst.gt_boxes).clone()
+        gt[:, 0::2] *= 1 / W
+        gt[:, 1::2] *= 1 / H
+        boxes = gt[idx]
+        colors = cl[:len(idx)]
+        boxed = draw(inp["image"], (boxes * H).cpu().numpy(), colors)
+        p, lab = make_system_prompt(processor, device, ignore_index)
+        n = len(names)
+        answer = (f"Sure, it is {classesboxes2string(names, boxes)}. There is an object in the image." if n == 1
+                  else f"Sure, it is {classesboxes2string(names, boxes)}. There are {n} objects in the image.")
+        p, lab = make_and_add_prompt_and_label(
+            p, lab, "provide multiple object names with their numbering index and the objects' bounding box "
+                    "coordinates in the image.", answer, processor, device, ignore_index)
+        answer = (f"Sure, it is {list2string(colors)} color. There is a bounding box in the image." if n == 1
+                  else f"Sure, it is {list2string(colors)} color. There are {n} bounding boxes in the image.")
+        p, lab = make_and_add_prompt_and_label(p, lab, "provide multiple bounding box colors in the image.", answer,
+                                               processor, device, ignore_index)
+        dice = torch.randint(high=2, low=0, size=(1,)).item()
+        pick = torch.randint(high=len(uniq), low=0, size=(1,)).item()
+        sel_cls = uniq_names[pick]
+        sel = torch.where(cls_ids == uniq[pick])[0]
+        sel_names = [names[i.item()] for i in sel]
+        sel_boxes = boxes[sel]
+        sel_colors = [cl[i.item()] for i in sel]
+        m = len(sel_names)
+        tail = "There is a bounding box in the image." if m == 1 else f"There are {m} bounding boxes in the image."
+        if dice == 0:
+            qa = (f"provide multiple bounding box colors corresponding {sel_cls} in the image.",
+                  f"Sure, it is {classescolors2string(sel_names, sel_colors)} color. {tail}")
+        else:
+            qa = (f"provide multiple bounding box coordinates for {sel_cls} in the image.",
+                  f"Sure, it is {classesboxes2string(sel_names, sel_boxes)} color. {tail}")
+        p, lab = make_and_add_prompt_and_label(p, lab, *qa, processor, device, ignore_index)
+        for r_int in torch.randperm(len(boxes))[:fix_num]:
+            name, box, color = names[r_int], boxes[r_int], cl[r_int]
+            if torch.randint(high=2, low=0, size=(1,)).item() == 0:
+                qa = (f"provide a bounding box coordinate of {color} bounding box color.",
+                      f"Sure, it is {box2string(box)}. There is a {color} bounding box color")
+            else:
+                qa = (f"provide a bounding box color of bounding box coordinate {box2string(box)}.",
+                      f"Sure, it is {color} color.")
+            p, lab = make_and_add_prompt_and_label(p, lab, *qa, processor, device, ignore_index)
+            if torch.randint(high=2, low=0, size=(1,)).item() == 0:
+                qa = (f"provide an object name for bounding box coordinate {box2string(box)}.", f"Sure, it is {name}.")
+            else:
+                qa = (f"provide an object name for {color} bounding box.", f"Sure, it is {name}.")
+            p, lab = make_and_add_prompt_and_label(p, lab, *qa, processor, device, ignore_index)
+        images.append(boxed)
+        prompts.append(p)
+        labels.append(lab)
+    if not prompts:
+        return {"input_ids": None}
+    return _finish(prompts, labels, images, processor, device, ignore_index)
 
 
 def eval_process(images, aux_prompt=None, prompt=None, processor=None, device=None, ignore_index=-100):

@@ -241,6 +241,29 @@ int cullavo_clip_image_preprocess(const uint8_t* images, int B, int C, int H, in
                                   float std0, float std1, float std2, uint8_t* tmp, void* out,
                                   int out_dtype, void* stream);
 
+/* ---- box drawing (data step: step-1 prompts and step-2 records with boxes) -----------------
+ * Replaces detectron2's Visualizer(img); _default_font_size = 16;
+ * overlay_instances(boxes=..., assigned_colors=...).get_image() in the reference's prompt builders
+ * (cullavo/arch_cullavo.py:149-153, :441-448): the image as a matplotlib Agg canvas shows it
+ * (imshow "nearest" on a (W+0.01) x (H+0.01) figure) with one 4 pt, alpha 0.5 stroked Rectangle
+ * per box, pixel-identical to matplotlib 3.10.8 (oracle/boxdraw_oracle.py).
+ * cullavo_visimage_geometry (host only, no GPU): rows[H] / cols[W] = source pixel of every canvas
+ * pixel; trans4 = matplotlib's transData (sx, tx, sy, ty; display y up) for the boxes.
+ * cullavo_draw_boxes: images uint8 [B, 3, H, W] at element strides sb/sc/sy/sx; boxes f32
+ * [B, max_boxes, 4] (x0, y0, x1, y1 in image pixels) already in draw order (largest area first,
+ * np.argsort(-areas) like overlay_instances), nbox[B] boxes used per image; colors uint8
+ * [B, max_boxes, 3]; width_px = max(font_size / 4, 1) pt at 100 dpi; alpha8 = round(alpha * 255);
+ * workspace of cullavo_draw_boxes_workspace(B, max_boxes) bytes (its first int32 is set non-zero
+ * when a box's outline or cells overflow the kernel's fixed capacity); out uint8 [B, 3, H, W]
+ * contiguous. W <= 8192. */
+int cullavo_visimage_geometry(int H, int W, int32_t* rows, int32_t* cols, double* trans4);
+size_t cullavo_draw_boxes_workspace(int B, int max_boxes);
+int cullavo_draw_boxes(const uint8_t* images, int B, int C, int H, int W, int64_t sb, int64_t sc, int64_t sy,
+                       int64_t sx, const int32_t* rows, const int32_t* cols, const float* boxes,
+                       const int32_t* nbox, const uint8_t* colors, int max_boxes, double td_sx, double td_tx,
+                       double td_sy, double td_ty, double width_px, int alpha8, void* workspace, uint8_t* out,
+                       void* stream);
+
 /* ---- embeddings / merge ------------------------------------------------------------------ */
 /* get_input_embeddings()(input_ids) (reference cullavo/arch_cullavo.py:582) */
 int cullavo_embedding_fwd(const int64_t* ids, int64_t n, const void* table, int64_t vocab,

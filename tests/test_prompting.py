@@ -74,10 +74,12 @@ def test_supervised_tokens_follow_the_answers():
     assert out["labels"].shape[1] == out["input_ids"].shape[1] + 575
 
 
-def test_box_records_raise_and_helpers():
+def test_box_records_need_an_image_and_helpers():
     from cullavo_amd import prompting as P
-    with pytest.raises(NotImplementedError):
-        P.step2_process([dict(GOLD["records"][0], boxes=[[0, 0, 1, 1]])], _processor(), "cpu")
+    # a record with boxes but no image fails like the reference's batch['image'] (:442)
+    with pytest.raises(KeyError):
+        P.step2_process([dict(GOLD["records"][0], boxes=[[0, 0, 1, 1]])], _processor(), "cpu",
+                        draw=lambda img, b, c: img)
     assert P.list2string(["red", "blue", 3]) == "red, blue, 3"
     assert P.box2string(torch.tensor([0.12345, 0.5, 1.0, 0.0004])) == "[0.123, 0.500, 1.000, 0.000]"
 
