@@ -112,7 +112,8 @@ def vit_main(args):
                                    f"{100 * top['ms'] / (elapsed * 1e3):.1f} % of the time at "
                                    f"{top['achieved_tflops']:.0f} TFLOP/s)",
                          "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None},
+                         "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "library_ceiling": gemm_ceiling(top) if world == 1 else None},
             "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share": round(f["ms"] / (elapsed * 1e3), 4),
                               "achieved_tflops": round(f["achieved_tflops"], 1)} for f in fams[:4]],
         }
@@ -254,6 +255,43 @@ def measured_traffic(kname):
     return None, None
 
 
+def gemm_ceiling(fam, iters=10):
+    """hipBLASLt (torch.matmul, same layouts) against this kernel on the family's largest shape,
+    same process, random bf16 operands: the measured library ceiling BASELINE.md §2 asks for"""
+    import torch
+
+    from cullavo_amd import ops
+    (M, N, K) = max(fam["shapes"], key=lambda s: s[0] * s[1] * s[2])
+    al, bl = next(k for k, v in GEMM_ROLE.items() if v == fam["role"])
+    g = torch.Generator(device="cuda").manual_seed(0)
+    A = torch.randn((K, M) if al else (M, K), device="cuda", generator=g).bfloat16()
+    B = torch.randn((K, N) if bl else (N, K), device="cuda", generator=g).bfloat16()
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    Am = A.t() if al else A
+    Bm = B if bl else B.t()  # [K, N]
+
+    def ours():
+        ops.gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N)
+
+    def lib():
+        torch.matmul(Am, Bm, out=C)
+
+    res = {}
+    for name, fn in (("ours", ours), ("hipblaslt", lib), ("ours2", ours), ("hipblaslt2", lib)):
+        fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
+        res[name] = 2.0 * M * N * K / (s.elapsed_time(e) / iters * 1e-3) / 1e12
+    del A, B, C
+    return {"shape": f"{M}x{N}x{K}", "layouts": [al, bl],
+            "this_kernel_tflops": round(max(res["ours"], res["ours2"]), 1),
+            "hipblaslt_tflops": round(max(res["hipblaslt"], res["hipblaslt2"]), 1)}
+
+
 def main():
     args = parse()
     if args.workload == "vit":
@@ -369,6 +407,8 @@ def main():
                               "achieved_tflops": round(f["achieved_tflops"], 1),
                               "frac": round(f["achieved_tflops"] / PEAK_BF16_TFLOPS, 4)} for f in fams[:6]],
         }
+        if world == 1:
+            line["roofline"]["library_ceiling"] = gemm_ceiling(top)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -148,8 +148,13 @@ DEV float act_apply(int act, float x) {
     // CLIP quick_gelu x * sigmoid(1.702 x) (tf:activations.py:117-123) as the reference's bf16
     // tensors evaluate it: the product 1.702 x and the sigmoid each round to bf16, the final
     // product rounds in the store
+    // exp and reciprocal by the hardware approximations (v_exp_f32, v_rcp_f32: ~1 ulp in f32),
+    // which the bf16 rounding of the sigmoid absorbs except within ~1 ulp of a bf16 tie; the
+    // IEEE division sequence made this epilogue a third of the ViT fc1 GEMM
+    // (tools/vit_gemm_bench.py)
     const float t = round_bf(1.702f * x);
-    const float sg = round_bf(1.f / (1.f + __expf(-t)));
+    const float e = __builtin_amdgcn_exp2f(t * -1.4426950408889634f);
+    const float sg = round_bf(__builtin_amdgcn_rcpf(1.f + e));
     return sg * x;
   }
   return x;

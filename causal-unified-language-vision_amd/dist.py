@@ -32,9 +32,11 @@ from .arena import ParamArena
 
 class GradReducer:
     def __init__(self, arenas: list[ParamArena], order: list[list[str]] | None = None, *,
-                 bucket_bytes: int = 256 << 20, group=None, use_side_stream: bool = True):
+                 bucket_bytes: int = 256 << 20, group=None, use_side_stream: bool = True,
+                 enabled: bool | None = None):
         """arenas: trainable arenas, in the order backward produces them; each arena's keys in
-        reverse offset order (decoder layer L-1 first)."""
+        reverse offset order (decoder layer L-1 first). enabled: None = only when the group has
+        more than one rank; True runs the exchange at world size 1 too (tests of the RCCL path)."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.buckets: list[dict] = []
@@ -58,7 +60,7 @@ class GradReducer:
         self.arenas = arenas
         dev = arenas[0].flat.device if arenas else torch.device("cpu")
         self.stream = torch.cuda.Stream(device=dev) if (use_side_stream and dev.type == "cuda") else None
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 if enabled is None else (bool(enabled) and dist.is_initialized())
         self.reset()
 
     def _add_bucket(self, ai, ar, keys):

@@ -240,3 +240,57 @@ def test_dp_step_equals_mean_of_single_gpu_grads(text_only_rank):
             err = (got - ref[name]).norm() / (ref[name].norm() + 1e-12)
             assert err < 1e-2, (name, r, err.item())
     torch.testing.assert_close(torch.from_numpy(out[0][0]["layers"]), torch.from_numpy(out[1][0]["layers"]))
+
+
+def _rccl_worker(port, q):
+    import sys
+    sys.path.insert(0, REPO)
+    try:
+        torch.cuda.set_device(0)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        from oracle import cullavo_oracle as O
+        from cullavo_amd.arch_cullavo import CuLLaVOModel
+        from cullavo_amd.config import tiny_gpu
+        from cullavo_amd.dist import GradReducer
+        cfg_o = O.config_small_gpu()
+        W = O.make_weights(cfg_o, 5)
+        ids, mask, pix, labels = (t.cuda() for t in O.make_inputs(cfg_o, 2, 40, 4, 50))
+        grads = []
+        for use_reducer in (False, True):
+            m = CuLLaVOModel(tiny_gpu(), device="cuda", trainable="full", init="none")
+            m.load_state_dict(W)
+            arenas = [a for a in m.arenas.values() if a.trainable]
+            red = GradReducer(arenas, bucket_bytes=64 << 10, enabled=True) if use_reducer else None
+            m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels).loss.backward()
+            if red is not None:
+                assert red.avg_supported and red.stream is not None
+                red.finish()
+            else:
+                for a in arenas:
+                    a.finalize_grads()
+            torch.cuda.synchronize()
+            grads.append({a.name: a.grad_flat.float().cpu() for a in arenas})
+        q.put(("ok", grads))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((traceback.format_exc(), None))
+
+
+@pytest.mark.gpu
+def test_rccl_reducer_path_world1_is_identity():
+    """The reducer's RCCL branch (ReduceOp.AVG, async all-reduce on the side stream, fixed bucket
+    order, stream join) on a real RCCL communicator: at world size 1 the averaged gradients must be
+    bitwise the local ones (the multi-rank arithmetic is covered by the gloo tests above)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    status, grads = q.get(timeout=600)
+    p.join(timeout=60)
+    assert status == "ok", status
+    plain, reduced = grads
+    for name in plain:
+        assert torch.equal(plain[name], reduced[name]), name
