@@ -16,6 +16,8 @@ per step by the fused backward Functions, so a bucket is just a slice of that bu
    rank pairs the same buffers in the same collective sequence even when their backward
    passes write parameters in different orders (a rank whose batch has no image writes the
    projector only when its unwritten gradients are zeroed at the end of the backward);
+ * weight-gradient GEMMs may run on their own side stream (functions.DW_STREAM): the comm
+   stream also waits for that stream before each bucket;
  * finish() zero-commits what the backward did not write (arena.finalize_grads), launches
    the remaining buckets and makes the compute stream wait for the comm stream, so the
    optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics.
@@ -101,13 +103,17 @@ class GradReducer:
         b["launched"] = True
         ar = self.arenas[b["arena"]]
         view = ar.grad_flat[b["lo"]:b["hi"]]
+        from .functions import dw_join, dw_wait
         if self.stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(view.device))
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
+                dw_wait(self.stream)  # weight gradients of the bucket may be on the dW side stream
                 b["work"] = self._allreduce(view)
         else:
+            if view.is_cuda:
+                dw_join(view.device)
             b["work"] = self._allreduce(view)
         self.launched.append(bi)
 

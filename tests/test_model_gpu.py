@@ -160,6 +160,34 @@ def test_kmajor_weight_copies_bitwise_and_refreshed(monkeypatch):
             assert torch.equal(a, b), f"mode {mode} step {s}"
 
 
+def test_dw_side_stream_bitwise(monkeypatch):
+    """Weight-gradient GEMMs on the side stream (functions.DW_STREAM "side") give gradients and
+    AdamW updates bitwise equal to the single-stream path, read on the compute stream right
+    after backward() with no device sync (the end-of-backward join orders them), including an
+    accumulating second micro-batch (beta = 1 writes)."""
+    import cullavo_amd.functions as FN
+    from cullavo_amd.optim import FusedAdamW
+    ids, mask, pix, labels = inputs()
+    ids2, mask2, pix2, labels2 = inputs(seed=5)
+    res = {}
+    for mode in ("off", "side"):
+        monkeypatch.setattr(FN, "DW_STREAM", mode)
+        m = build()
+        opt = FusedAdamW(list(m.arenas.values()), lr=1e-3)
+        seen = []
+        for step in range(2):
+            opt.zero_grad()
+            for (a, b, c, d) in ((ids, mask, pix, labels), (ids2, mask2, pix2, labels2)):
+                out = m(input_ids=a, pixel_values=c, attention_mask=b, labels=d)
+                out.loss.backward()
+                seen.append(torch.cat([ar.grad_flat.clone() for ar in m.arenas.values() if ar.trainable]))
+            opt.step()
+        seen.append(torch.cat([ar.flat.clone() for ar in m.arenas.values()]))
+        res[mode] = seen
+    for i, (a, b) in enumerate(zip(res["off"], res["side"])):
+        assert torch.equal(a, b), i
+
+
 def test_adamw_skips_parameters_without_gradient():
     """A text-only batch never reaches the projector: like torch.optim.AdamW on a parameter
     whose .grad is None, FusedAdamW leaves it (and its step count) untouched, while the
