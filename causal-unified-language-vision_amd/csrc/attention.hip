@@ -591,13 +591,13 @@ struct StageN {
   }
 };
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DS_OUT = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
     const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
     const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
     int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
-    const int32_t* __restrict__ kv_start) {
+    const int32_t* __restrict__ kv_start, u16* __restrict__ dST, int64_t ldst, int64_t st_bh) {
   constexpr int QT = 64, KB = 128;
   constexpr int TQ = QT * D * 2;          // bytes of a Q (or dO) tile
   constexpr int TK = KB * D * 2;          // bytes of the K (or V) image
@@ -701,6 +701,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     for (int s = 0; s < 2; ++s) {
       const frag8 pf = pack_frag(sacc, s);
       const frag8 df = pack_frag(pacc, s);
+      if (DS_OUT) {
+        // dS^T[key][q] (the bf16 operand of dK) for the dQ kernel: registers 8s..8s+3 / 8s+4..8s+7
+        // are query rows 16s + 4hf + 0..3 / 16s + 8 + 4hf + 0..3 of this wave's 32
+        const u16x8 w = __builtin_bit_cast(u16x8, df);
+        u16* row = dST + ((int64_t)b * H + h) * st_bh + (int64_t)key * ldst + qt * QT + 32 * u + 16 * s + 4 * hf;
+        *reinterpret_cast<u16x4*>(row) = u16x4{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<u16x4*>(row + 8) = u16x4{w[4], w[5], w[6], w[7]};
+      }
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt) {
         dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TQ, 32 * u + 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
@@ -857,6 +865,303 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq8_k(
   }
 }
 
+// ============================================================================================
+// backward dK/dV, 64 keys per wave
+// ============================================================================================
+// One workgroup = 4 waves (one per SIMD, so up to 512 registers each) = 256 keys of one
+// (b, h). A wave keeps the K fragments of its 64 keys (two 32-key MFMA tiles) in registers,
+// their V rows in an LDS image and their dK / dV in 256 accumulator registers while the
+// workgroup sweeps 32-row Q / dO slices staged in LDS; every Q / dO row fragment and every
+// transposed fragment read from LDS feeds the MFMAs of both key tiles: 32 KiB of LDS reads
+// per 64 MFMAs per wave, against 48 KiB per 32 in the 8-wave kernel above, whose re-read K / V
+// rows made it LDS-bound (V in registers too spills at D = 128)
+// (cdna_hip_programming.md "Attention backward": key on the lane, dK / dV held in
+// accumulators over the whole sweep, no sum across workgroups).
+// Work order: key block kb = blockIdx / (B*H), so every (b, h)'s heaviest causal block (the
+// longest query sweep) is dispatched first and the one-block-per-CU rounds end together.
+// A wave whose 64 keys all lie after a slice's last query (causal diagonal) skips it.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w64_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
+    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
+    const int32_t* __restrict__ kv_start) {
+  constexpr int QT = 32, KB = 256, J = 2;
+  constexpr int TQ = QT * D * 2;            // bytes of a Q (or dO) slice
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int BUF = 2 * TQ + 2 * QT * 4;  // [Q | dO | lse*log2e (32) | delta (32)]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sV = smem + 2 * BUF;                // V image of the block's 256 keys
+
+  const int nkb = (Lk + KB - 1) / KB;
+  const int BH = (int)gridDim.x / nkb;
+  const int kb = (int)blockIdx.x / BH, hb = (int)blockIdx.x % BH;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int kw = kb * KB + wave * 64;  // first key of this wave
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
+  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
+
+  frag8 kf[J][NS];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int key = kw + 32 * j + (lane & 31);
+    const bool ok = key < Lk;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      kf[j][s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Kb + (int64_t)key * ldk + 16 * s + 8 * hf) : u16x8(0));
+  }
+  f32x16 dk[J][ND], dv[J][ND];
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) { dk[j][i] = f32x16(0.f); dv[j][i] = f32x16(0.f); }
+  const float c = scale * kLog2e;
+
+  const int kmin = kb * KB;
+  const int qt0 = CAUSAL ? (kmin / QT) : 0;
+  const int nqt = (Lq + QT - 1) / QT;
+  const bool block_live = kmin < Lk && (kmin + KB > kstart);
+
+  StageN<QT, D, 256> sq, sdo;
+  float aux = 0.f;
+  auto load_aux = [&](int qt) {
+    if (threadIdx.x < 2 * QT) {
+      const int qq = qt * QT + (int)threadIdx.x % QT;
+      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] * kLog2e : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+    }
+  };
+  auto store_aux = [&](char* buf) {
+    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TQ))[threadIdx.x] = aux;
+  };
+  if (block_live) {
+#pragma unroll
+    for (int part = 0; part < KB / 64; ++part) {
+      StageN<64, D, 256> sv;
+      sv.load(Vb, ldv, kmin + 64 * part, Lk);
+      sv.store(sV + 64 * part * D * 2);
+    }
+  }
+  if (block_live && qt0 < nqt) {
+    sq.load(Qb, ldq, qt0 * QT, Lq);
+    sdo.load(dOb, lddo, qt0 * QT, Lq);
+    sq.store(smem);
+    sdo.store(smem + TQ);
+    load_aux(qt0);
+    store_aux(smem);
+  }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
+  __syncthreads();
+
+  // slices that end before this wave's first key (causal diagonal) only stage and sync: the
+  // same barrier count as the other waves, no branch around the MFMA body (a branch there
+  // makes hipcc spill the 256 accumulators' neighbours)
+  const int nq = block_live ? nqt : qt0;
+  const int qskip = CAUSAL ? min(nq, max(qt0, kw / QT)) : qt0;
+  int qt = qt0;
+  for (; qt < qskip; ++qt) {
+    char* nbuf = smem + ((qt - qt0 + 1) & 1) * BUF;
+    const bool more = qt + 1 < nqt;
+    if (more) {
+      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
+      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+      load_aux(qt + 1);
+      sq.store(nbuf);
+      sdo.store(nbuf + TQ);
+      store_aux(nbuf);
+    }
+    __syncthreads();
+  }
+  for (; qt < nq; ++qt) {
+    const int cur = (qt - qt0) & 1;
+    char* buf = smem + cur * BUF;
+    char* nbuf = smem + (cur ^ 1) * BUF;
+    const bool more = qt + 1 < nqt;
+    if (more) {
+      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
+      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+      load_aux(qt + 1);
+    }
+    const int q0 = qt * QT;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // lane-derived LDS addresses: recomputed per slice, not hoisted
+    {
+      const float* slse = (const float*)(buf + 2 * TQ);
+      const float* sdel = slse + QT;
+      // S[q][key], dP[q][key] of both key tiles; one Q / dO row fragment per k-step
+      f32x16 sacc[J], pacc[J];
+#pragma unroll
+      for (int j = 0; j < J; ++j) { sacc[j] = f32x16(0.f); pacc[j] = f32x16(0.f); }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const frag8 qa = row_frag<D>(buf, 0, s, ln);
+        const frag8 oa = row_frag<D>(buf + TQ, 0, s, ln);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+          sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[j][s], sacc[j], 0, 0, 0);
+          pacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, row_frag<D>(sV, wave * 64 + 32 * j, s, ln), pacc[j], 0, 0, 0);
+        }
+      }
+      // P = exp2(S*c - lse*log2e), dS = P * (dP - delta); masks only where a bound crosses
+      const bool need_mask = (CAUSAL && kw + 63 > q0) || kw + 64 > Lk || kw < kstart || q0 + QT > Lq;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 8 * rr + 4 * hf);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 8 * rr + 4 * hf);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = rr * 4 + jj;
+          const int qq = q0 + 8 * rr + 4 * hf + jj;
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            float pv = fast_exp2(fmaf(sacc[j][r], c, -l4[jj]));
+            if (need_mask) {
+              const int key = kw + 32 * j + (lane & 31);
+              if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
+            }
+            sacc[j][r] = pv;
+            pacc[j][r] = pv * (pacc[j][r] - d4[jj]);
+          }
+        }
+      }
+      // dV += P^T dO ; dK += dS^T Q: each transposed dO / Q fragment serves both key tiles
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        frag8 pf[J], df[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) { pf[j] = pack_frag(sacc[j], s); df[j] = pack_frag(pacc[j], s); }
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const frag8 tdo = tr_frag<D>(buf + TQ, 16 * s, dt * 32, ln);
+          const frag8 tq = tr_frag<D>(buf, 16 * s, dt * 32, ln);
+#pragma unroll
+          for (int j = 0; j < J; ++j) {
+            dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[j], tdo, dv[j][dt], 0, 0, 0);
+            dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df[j], tq, dk[j][dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (more) {
+      sq.store(nbuf);
+      sdo.store(nbuf + TQ);
+      store_aux(nbuf);
+    }
+    __syncthreads();
+  }
+
+  // dK/dV[key][d]: register r = key row, lane = d column
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kw + 32 * j + acc_row(r, hf);
+        if (kk < Lk) {
+          const int d = dt * 32 + (lane & 31);
+          dK[((int64_t)b * Lk + kk) * lddk + (int64_t)h * D + d] = f2bf(dk[j][dt][r] * scale);
+          dV[((int64_t)b * Lk + kk) * lddv + (int64_t)h * D + d] = f2bf(dv[j][dt][r]);
+        }
+      }
+}
+
+// ============================================================================================
+// backward dQ from the stored dS (mode 7)
+// ============================================================================================
+// The 8-wave dK/dV kernel writes dS^T[b, h][key][q] (bf16, the same rounded values its dK
+// product consumes) for every (key, query) pair it visits; dQ^T = K^T dS^T then needs no S / dP
+// recompute: one product instead of three. A wave owns 32 query columns, the workgroup sweeps
+// 64-key tiles up to the causal diagonal with K and dS^T tiles staged in LDS, both operands
+// read as transposed fragments (the same k order on both sides). dS^T has LkP =
+// round_up(Lk, 128) rows (keys) of LqP = round_up(Lq, 128) queries (cullavo_attn_bwd_workspace).
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict__ K, int64_t ldk,
+                                                           const u16* __restrict__ dST, int64_t ldst, int64_t st_bh,
+                                                           int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
+                                                           int Lq, int Lk, float scale,
+                                                           const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 64, QB = 128;
+  constexpr int TK = KT * D * 2, TS = KT * QB * 2, BUF = TK + TS;
+  constexpr int NS = KT / 16, ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (Lq + QB - 1) / QB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * QB;
+
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = f32x16(0.f);
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * QB + QB);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  StageN<KT, D, 256> sk;
+  StageN<KT, QB, 256> ss;
+  if (t0 < ntiles) {
+    sk.load(Kb, ldk, t0 * KT, Lk);
+    ss.load(Sb, ldst, t0 * KT, LkP);
+    sk.store(smem);
+    ss.store(smem + TK);
+  }
+  __builtin_amdgcn_s_waitcnt(kVmcnt0);
+  __syncthreads();
+  for (int t = t0; t < ntiles; ++t) {
+    char* bK = smem + ((t - t0) & 1) * BUF;
+    char* bS = bK + TK;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      sk.load(Kb, ldk, (t + 1) * KT, Lk);
+      ss.load(Sb, ldst, (t + 1) * KT, LkP);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const frag8 bs = tr_frag<QB>(bS, 16 * s, wave * 32, lane);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bK, 16 * s, dt * 32, lane), bs, dq[dt], 0, 0, 0);
+    }
+    if (more) {
+      char* nK = smem + ((t - t0 + 1) & 1) * BUF;
+      sk.store(nK);
+      ss.store(nK + TK);
+    }
+    __syncthreads();
+  }
+  if (q < Lq) {
+    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[dt][rr * 4 + j] * scale);
+        *reinterpret_cast<u16x4*>(dQb + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+  }
+}
+
+int64_t ds_rows(int Lk) { return cdiv(Lk, 128) * 128; }
+int64_t ds_cols(int Lq) { return cdiv(Lq, 128) * 128; }
+
 template <typename Kern>
 void set_smem(Kern k, int bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -919,13 +1224,61 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
     once = true;
   }
   attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks);
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
   if (DQ8)
     attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
   else
     attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
+  return cullavo_check_launch("attn_bwd");
+}
+
+// mode 7: the 8-wave dK/dV kernel storing dS^T + dQ from it (workspace: B*H*LkP*LqP bf16)
+template <int D, bool CAUSAL>
+int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
+                  int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
+                  u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
+                  const int32_t* ks, u16* ds, hipStream_t s) {
+  const int64_t rows = (int64_t)B * Lq * H;
+  attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
+  const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
+  const int smem_b = 2 * (64 * D * 2 + 64 * 128 * 2);
+  static bool once = false;
+  if (!once) {
+    set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true>, smem_a);
+    set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
+    once = true;
+  }
+  const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
+  attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
+  attn_bwd_dq_ds_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+      k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+  return cullavo_check_launch("attn_bwd");
+}
+
+
+// mode 6: the 64-keys-per-wave dK/dV kernel + the 4-wave 32-key dQ kernel
+template <int D, bool CAUSAL>
+int bwd64_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
+                 int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
+                 u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
+                 const int32_t* ks, hipStream_t s) {
+  const int64_t rows = (int64_t)B * Lq * H;
+  attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
+  const int smem_a = 2 * (2 * 32 * D * 2 + 2 * 32 * 4) + 256 * D * 2;
+  const int smem_b = 4 * 32 * D * 2;
+  static bool once = false;
+  if (!once) {
+    set_smem(attn_bwd_dkdv_w64_k<D, CAUSAL>, smem_a);
+    set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
+    once = true;
+  }
+  attn_bwd_dkdv_w64_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 256) * H * B), 256, smem_a, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks);
+  attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
@@ -938,7 +1291,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
   const int prev = g_bwd_tiles;
-  if (mode >= -1 && mode <= 5) g_bwd_tiles = mode;
+  if (mode >= -1 && mode <= 7) g_bwd_tiles = mode;
   return prev;
 }
 
@@ -966,11 +1319,31 @@ extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64
                 : fwd_launch<64, false>(Q, ldq, K, ldk, V, ldv, O, ldo, lse, B, H, Lq, Lk, scale, kv_start, s);
 }
 
+// default: D=128 (the LM) mode 7 -- in the 7B shape 532 us per layer against 667 for mode 4
+// (tools/attn_bench.py), the dQ kernel no longer recomputes S and dP; D=64 (the ViT) mode 2
+static int bwd_mode(int D) { return g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 7 : 2); }
+
+extern "C" size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype) {
+  if (dtype != CULLAVO_DT_BF16 || D < 64 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || bwd_mode(D) != 7) return 0;
+  return (size_t)B * H * ds_rows(Lk) * ds_cols(Lq) * 2;
+}
+
 extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                                 int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
                                 const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                                 int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                                 float scale, int causal, const int32_t* kv_start, int dtype, void* stream) {
+  return cullavo_attn_bwd_ws(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, delta, dq, lddq, dk, lddk, dv, lddv,
+                             B, H, Lq, Lk, D, scale, causal, kv_start, dtype, nullptr, 0, stream);
+}
+
+extern "C" int cullavo_attn_bwd_ws(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                   int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                                   const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
+                                   int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
+                                   float scale, int causal, const int32_t* kv_start, int dtype, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+
   CV_REQUIRE(dtype == CULLAVO_DT_BF16 || dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "attention: bf16 / f32");
   CV_REQUIRE(D == 16 || D == 32 || D == 64 || D == 128, CULLAVO_EUNSUPPORTED, "head_dim must be 16, 32, 64 or 128");
   CV_REQUIRE(!causal || Lq == Lk, CULLAVO_EINVAL, "causal attention needs Lq == Lk");
@@ -991,7 +1364,23 @@ extern "C" int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64
   // D=64 (the ViT) the 4-wave kernels with 32-row dK/dV and 64-key dQ tiles (647 vs 797 us at
   // B=64, T=577, H=16): there the 4-wave kernels already hold K/V in registers at < 256
   // VGPRs and the 8-wave LDS re-reads cost more than the second wave hides (tools/attn_bench.py)
-  const int mode = g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 4 : 2);
+  int mode = bwd_mode(D);
+  if (mode == 7) {
+    if (workspace != nullptr && workspace_bytes >= cullavo_attn_bwd_workspace(B, H, Lq, Lk, D, dtype)) {
+      u16* ds = (u16*)workspace;
+#define BDS(DD, CC) bwd_ds_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, ds, s)
+      if (D == 128) return causal ? BDS(128, true) : BDS(128, false);
+      return causal ? BDS(64, true) : BDS(64, false);
+#undef BDS
+    }
+    mode = 4;  // no dS workspace: the recompute path (same dK / dV kernel)
+  }
+  if (mode == 6) {
+#define B64(DD, CC) bwd64_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+    if (D == 128) return causal ? B64(128, true) : B64(128, false);
+    return causal ? B64(64, true) : B64(64, false);
+#undef B64
+  }
   if (mode == 4 || mode == 5) {
 #define B8(DD, CC, Q8) bwd8_launch<DD, CC, Q8>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
     if (mode == 5) {

@@ -355,9 +355,11 @@ def attn_bwd(q, k, v, o, do, lse, *, B: int, H: int, Lq: int, Lk: int, D: int, s
     dk = dk if dk is not None else torch.empty((B * Lk, H * D), dtype=q.dtype, device=q.device)
     dv = dv if dv is not None else torch.empty((B * Lk, H * D), dtype=q.dtype, device=q.device)
     delta = torch.empty((B, H, Lq), dtype=torch.float32, device=q.device)
-    call("attn_bwd", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(o), _ld(o), _ptr(do), _ld(do),
+    nbytes = lib().cullavo_attn_bwd_workspace(B, H, Lq, Lk, D, _dt(q))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device) if nbytes else None
+    call("attn_bwd_ws", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(o), _ld(o), _ptr(do), _ld(do),
          _ptr(lse), _ptr(delta), _ptr(dq), _ld(dq), _ptr(dk), _ld(dk), _ptr(dv), _ld(dv), B, H, Lq, Lk, D,
-         float(scale), int(causal), _ptr(kv_start), _dt(q), _stream())
+         float(scale), int(causal), _ptr(kv_start), _dt(q), _ptr(ws), nbytes, _stream())
     return dq, dk, dv
 
 

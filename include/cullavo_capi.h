@@ -196,10 +196,25 @@ int cullavo_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, con
                      const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
                      int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
                      float scale, int causal, const int32_t* kv_start, int dtype, void* stream);
+/* cullavo_attn_bwd with a scratch buffer: in mode 7 the dK/dV kernel stores dS^T (bf16,
+   [B*H][round_up(Lk,128)][round_up(Lq,128)]) there and dQ is one product over it instead of
+   a recompute of S and dP; workspace_bytes below what cullavo_attn_bwd_workspace returns (or
+   a null workspace) falls back to mode 4. Caller-owned, stream-ordered like every buffer. */
+int cullavo_attn_bwd_ws(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                        int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                        const float* lse, float* delta, void* dq, int64_t lddq, void* dk,
+                        int64_t lddk, void* dv, int64_t lddv, int B, int H, int Lq, int Lk, int D,
+                        float scale, int causal, const int32_t* kv_start, int dtype, void* workspace,
+                        size_t workspace_bytes, void* stream);
+/* bytes of workspace cullavo_attn_bwd_ws uses for this problem in the current mode (0: none) */
+size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype);
 /* Tuning/A-B switch for cullavo_attn_bwd: 4 = the 8-wave dK/dV kernel (two waves per SIMD;
    waves w and w+4 split each query tile and add their partial sums once, in a fixed order)
    with the 4-wave 32-key dQ kernel; 5 = both kernels 8-wave; 0-3 = the 4-wave kernels;
-   -1 (the default) = 4 for D=128, 2 for D=64 (measured per head dim).
+   6 = 64 keys per wave dK/dV (4 waves, one per SIMD; bitwise equal to 0-3); 7 = mode 4's dK/dV
+   kernel storing dS^T + dQ from it (needs the cullavo_attn_bwd_ws workspace);
+   -1 (the default) = 7 for D=128 (4 through cullavo_attn_bwd, which has no workspace), 2 for
+   D=64 (measured per head dim).
    In 0-3 with bit 0 = 64 query rows per dK/dV barrier, bit 1 = 64
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
    in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */

@@ -314,7 +314,8 @@ def test_attention_fwd_bwd(B, H, L, D, causal):
 @pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
 def test_attention_bwd_tile_modes_bitwise(D, causal):
     """Every backward tile shape (cullavo_attn_set_bwd_tiles) sums the same products in the same
-    order, so dQ/dK/dV agree bit for bit; ragged L and a left-padded batch row included."""
+    order, so dQ/dK/dV agree bit for bit; ragged L and a left-padded batch row included. Mode 6
+    (64 keys per wave) keeps mode 0's per-key product order and is bitwise equal to it too."""
     from cullavo_amd import _lib
     B, H, L = 2, 3, 200
     q, k, v, do = (rnd((B * L, H * D), s).to(DEV) for s in (91, 92, 93, 94))
@@ -324,27 +325,32 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
     prev = _lib.lib().cullavo_attn_set_bwd_tiles(0)
     try:
         outs = []
-        for mode in range(4):
+        for mode in (0, 1, 2, 3, 6):
             _lib.lib().cullavo_attn_set_bwd_tiles(mode)
             outs.append([t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)])
     finally:
         _lib.lib().cullavo_attn_set_bwd_tiles(prev)
-    for mode in range(1, 4):
-        for name, a, b in zip("qkv", outs[0], outs[mode]):
+    for i, mode in enumerate((1, 2, 3, 6)):
+        for name, a, b in zip("qkv", outs[0], outs[i + 1]):
             assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode {mode}"
     # mode 4 (8-wave kernels: the pair halves of each tile are summed once at the end) adds the
     # same products in another order: bf16-rounding-level differences only, and deterministic
-    for mode8 in (4, 5):
+    res8 = {}
+    for mode8 in (4, 5, 7):
         _lib.lib().cullavo_attn_set_bwd_tiles(mode8)
         try:
             o4 = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
             o4b = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
         finally:
             _lib.lib().cullavo_attn_set_bwd_tiles(prev)
+        res8[mode8] = o4
         for name, a, b, c in zip("qkv", outs[0], o4, o4b):
             assert torch.equal(b.view(torch.int16), c.view(torch.int16)), f"d{name} mode {mode8} not deterministic"
             err = ((a.float() - b.float()).norm() / a.float().norm()).item()
             assert err <= 5e-3, (name, mode8, err)
+    # mode 7 runs mode 4's dK/dV kernel (plus the dS^T stores): dK, dV bitwise equal to it
+    for name, a, b in zip("kv", res8[4][1:], res8[7][1:]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode 7 vs 4"
 
 
 def test_attention_strided_and_kv_start():

@@ -32,7 +32,7 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
     tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
     res = []
     outs = {}
-    for mode in (4, 5, 1, 2):  # 4 / 5 = 8-wave dK/dV (+ 4- / 8-wave dQ), 1 / 2 = the 4-wave kernels
+    for mode in (4, 7, 1, 2):  # 4 = 8-wave dK/dV + 4-wave dQ, 7 = 8-wave dK/dV storing dS + dQ from it, 1 / 2 = 4-wave
         _lib.lib().cullavo_attn_set_bwd_tiles(mode)
         tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
                                          causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
@@ -40,6 +40,6 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
         outs[mode] = dqkv.float().clone()
         res.append(f"m{mode} {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.1f} TF")
     diff = ((outs[4] - outs[1]).norm() / outs[1].norm()).item()
-    res.append(f"rel(m4, m1) {diff:.1e}")
+    res.append(f"rel(m4, m1) {diff:.1e} rel(m7, m1) {((outs[7] - outs[1]).norm() / outs[1].norm()).item():.1e}")
     _lib.lib().cullavo_attn_set_bwd_tiles(-1)
     print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd " + " | ".join(res))
