@@ -617,6 +617,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   const int ksl = wave & 3, u = wave >> 2;          // 32-key slice, query half of each tile
   const int key = kb * KB + ksl * 32 + (lane & 31);  // this lane's key
   const int kstart = kv_start ? kv_start[b] : 0;
+  // live queries of this key: [qlo, qlim) (empty for keys before kstart or past Lk)
+  const int qlo = CAUSAL ? key : 0;
+  const int qlim = (key < kstart || key >= Lk) ? qlo : Lq;
+  const unsigned qspan = (unsigned)max(qlim - qlo, 0);
 
   const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
   const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
@@ -682,6 +686,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 32 * u, s, lane), row_frag<D>(sK, 32 * ksl, s, lane), sacc, 0, 0, 0);
       pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TQ, 32 * u, s, lane), row_frag<D>(sV, 32 * ksl, s, lane), pacc, 0, 0, 0);
     }
+    // query qq is live for this lane's key iff qlo <= qq < qlim: one unsigned compare per element
+    const int qoff = qt * QT + 32 * u + 4 * hf - qlo;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 32 * u + 8 * rr + 4 * hf);
@@ -689,9 +695,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = rr * 4 + j;
-        const int qq = qt * QT + 32 * u + 8 * rr + 4 * hf + j;
         float pv = fast_exp2(fmaf(sacc[r], c, -l4[j] * kLog2e));
-        if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
+        if ((unsigned)(qoff + 8 * rr + j) >= qspan) pv = 0.f;
         sacc[r] = pv;
         pacc[r] = pv * (pacc[r] - d4[j]);
       }
