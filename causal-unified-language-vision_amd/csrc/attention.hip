@@ -146,6 +146,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   float m = -INFINITY, l = 0.f;
   const float c = scale * kLog2e;
 
+  // live keys of this lane's query: [kstart, khi)
+  const int khi = CAUSAL ? min(Lk, q + 1) : Lk;
+  const unsigned kspan = (unsigned)max(khi - kstart, 0);
   int kend = Lk;
   if (CAUSAL) kend = min(Lk, qb * 128 + 128);
   const int ntiles = (kend + KT - 1) / KT;
@@ -187,14 +190,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     const int kbase = t * KT;
     const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
     if (need_mask) {
+      // key is live for this lane's query iff kstart <= key < khi: one unsigned compare
+      const int koff = kbase + 4 * hf - kstart;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kbase + kt * 32 + acc_row(r, hf);
-          const bool dead = key >= Lk || key < kstart || (CAUSAL && key > q);
-          st[kt][r] = dead ? -INFINITY : st[kt][r];
-        }
+        for (int r = 0; r < 16; ++r)
+          st[kt][r] = (unsigned)(koff + kt * 32 + acc_row(r, 0)) >= kspan ? -INFINITY : st[kt][r];
     }
     float tmax = -INFINITY;
 #pragma unroll
