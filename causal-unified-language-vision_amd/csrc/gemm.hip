@@ -14,6 +14,9 @@
 // Epilogue order mirrors the reference's bf16 module chain (see cullavo_capi.h).
 #include "common.h"
 
+#include <map>
+#include <mutex>
+
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64;
@@ -44,6 +47,11 @@ struct GemmArgs {
   int kt_per;         // K-tiles per split
   int epi_lds;        // 8-wave kernels: LDS-staged 16-B epilogue (all pointers 16-B aligned)
   int nt_store;       // C written with non-temporal stores (streamed past the caches)
+  // stream-K tail of the 8-wave kernels (sk_units = 0: off): blocks < sk_dp run whole tiles;
+  // the sk_units blocks after them split the sk_iters K-iterations of the remaining tiles evenly
+  int sk_dp, sk_units;
+  int64_t sk_iters;
+  float* sk_ws;       // f32 partials [sk_units][2][512 threads x TMW*TN f32x4], fragment order
 };
 
 template <typename V>
@@ -555,53 +563,30 @@ DEV frag8 read_frag_w(const char* lds, int rbase, int ks, int lane) {
 // LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
 // 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
 // partner wave's MFMAs instead of beside nothing).
-template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
-__global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
-  constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
+// One tile's K-tiles [kb, ke) into acc (zeroed here): LDS-DMA double buffer, one barrier per
+// K-tile, the MFMA loop of the 8-wave kernels (shared by the data-parallel and stream-K kernels)
+template <int AL, int BL, int BM2, int BN, int LDR, int TMW, int TN>
+DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int64_t m0,
+                      int64_t n0, int kb, int ke, char* smem, int wave, int lane, f32x4 (&acc)[TMW][TN]) {
   constexpr int TILE_A = BM2 * BK * 2;
   constexpr int TILE_B = BN * BK * 2;
   constexpr int STAGE = TILE_A + TILE_B;
-  constexpr int WN_COLS = BN / 4;     // per-wave N extent (4 waves across N)
-  constexpr int TN = WN_COLS / 16;    // 16-col MFMA tiles per wave
-  constexpr int TMW = BM2 / 32;       // 16-row MFMA tiles per wave (BM/2 rows)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * p.tiles_n;
-  const int group = lid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(p.tiles_m - first_m, GROUP_M);
-  const int tm_idx = first_m + (lid % per_group) % gsize;
-  const int tn_idx = (lid % per_group) / gsize;
-  const int64_t m0 = (int64_t)tm_idx * BM2, n0 = (int64_t)tn_idx * BN;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int WN_COLS = BN / 4;
   const int wm = wave >> 2, wn = wave & 3;
-
-  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
-  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
-
-  f32x4 acc[TMW][TN];
 #pragma unroll
   for (int i = 0; i < TMW; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)cdiv(p.K, BK);
-  dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, 0, p.K, smem, wave, lane);
-  dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, 0, p.K, smem + TILE_A, wave, lane);
+  dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, (int64_t)kb * BK, p.K, smem, wave, lane);
+  dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, (int64_t)kb * BK, p.K, smem + TILE_A, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    const bool more = kt + 1 < nk;
-    char* nxt = smem + ((kt + 1) & 1) * STAGE;
+  for (int kt = kb; kt < ke; ++kt) {
+    char* cur = smem + ((kt - kb) & 1) * STAGE;
+    const bool more = kt + 1 < ke;
+    char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
     const int64_t k1 = (int64_t)(kt + 1) * BK;
     // next K-tile's LDS-DMA pieces, all issued before this tile's MFMAs (issuing them one by
     // one between MFMA groups measured 5-15 % slower, profiles/r01/gemm_8phase.md)
@@ -647,6 +632,47 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+}
+
+// grouped, XCD-friendly tile order: virtual tile index -> (m0, n0)
+template <int BM2, int BN>
+DEV void tile_origin(const GemmArgs& p, int lid, int64_t& m0, int64_t& n0) {
+  constexpr int GROUP_M = 4;
+  const int per_group = GROUP_M * p.tiles_n;
+  const int group = lid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
+  n0 = (int64_t)((lid % per_group) / gsize) * BN;
+}
+
+// LDR selects which waves stage the next K-tile: 0 = all eight (each wave issues its share of
+// LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
+// 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
+// partner wave's MFMAs instead of beside nothing). Data-parallel blocks: one whole tile each,
+// the first sk_dp virtual tiles (all of them without a stream-K tail).
+template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
+__global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
+  constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
+  constexpr int WN_COLS = BN / 4;     // per-wave N extent (4 waves across N)
+  constexpr int TN = WN_COLS / 16;    // 16-col MFMA tiles per wave
+  constexpr int TMW = BM2 / 32;       // 16-row MFMA tiles per wave (BM/2 rows)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lid = xcd_remap(blockIdx.x, p.sk_dp);
+  int64_t m0, n0;
+  tile_origin<BM2, BN>(p, lid, m0, n0);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  f32x4 acc[TMW][TN];
+  tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, 0, (int)cdiv(p.K, BK), smem, wave, lane, acc);
 
   if constexpr (BN == 256) {
     if (p.epi_lds) {
@@ -662,6 +688,97 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
       const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
       store4<CT>(p, acc[tm][tn], m, n);
     }
+  }
+}
+
+// Stream-K blocks (launched after the data-parallel ones): block u takes iterations
+// [sk_iters*u/U, sk_iters*(u+1)/U) of the tail tiles (virtual tiles sk_dp.., nk iterations each).
+// A piece that covers a whole tile gets the normal epilogue; a partial piece writes f32 partial
+// sums in fragment order, slot 0 for the block's first piece, 1 for its last (only those two
+// can be partial).
+template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
+__global__ __launch_bounds__(512, 1) void gemm256_sk_k(GemmArgs p) {
+  constexpr int BM2 = BMT;
+  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16, TMW = BM2 / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
+
+  const int nk = (int)cdiv(p.K, BK);
+  const int unit = xcd_remap(blockIdx.x, p.sk_units);  // neighbouring shares (shared tiles) on one XCD
+  const int64_t base = (int64_t)p.sk_dp * nk;
+  const int64_t it0 = base + p.sk_iters * unit / p.sk_units;
+  const int64_t it1 = base + p.sk_iters * (unit + 1) / p.sk_units;
+  for (int64_t it = it0; it < it1;) {
+    const int kb = (int)(it % nk);
+    const int ke = (int)min((int64_t)nk, kb + (it1 - it));
+    int64_t m0, n0;
+    tile_origin<BM2, BN>(p, (int)(it / nk), m0, n0);
+    f32x4 acc[TMW][TN];
+    tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, kb, ke, smem, wave, lane, acc);
+    if (kb == 0 && ke == nk) {
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm) {
+        const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4);
+      }
+    } else {
+      float* w = p.sk_ws + ((int64_t)(unit * 2 + (it == it0 ? 0 : 1)) * TMW * TN * 512 + threadIdx.x) * 4;
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          *reinterpret_cast<f32x4*>(w + (int64_t)(tm * TN + tn) * 512 * 4) = acc[tm][tn];
+    }
+    it += ke - kb;
+  }
+}
+
+// Stream-K fix-up: one block per tail tile that more than one block worked on; adds the pieces'
+// f32 partials in K order (fixed, so results are reproducible) and runs the epilogue.
+template <int CT, int BM2, int BN>
+__global__ __launch_bounds__(512) void gemm_sk_fixup_k(GemmArgs p) {
+  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16, TMW = BM2 / 32;
+  const int64_t nk = cdiv(p.K, BK);
+  const int64_t I = p.sk_iters, U = p.sk_units;
+  const int64_t x0 = (int64_t)blockIdx.x * nk, x1 = x0 + nk - 1;  // the tile's iterations (tail-relative)
+  auto start = [&](int64_t u) { return I * u / U; };
+  auto unit_of = [&](int64_t x) {
+    int64_t u = x * U / I;
+    while (u > 0 && start(u) > x) --u;
+    while (u + 1 < U && start(u + 1) <= x) ++u;
+    return u;
+  };
+  const int64_t u0 = unit_of(x0), u1 = unit_of(x1);
+  if (u0 == u1) return;  // one block ran the whole tile and its epilogue
+  f32x4 acc[TMW][TN];
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t u = u0; u <= u1; ++u) {
+    if (start(u + 1) == start(u)) continue;  // an empty share
+    const int slot = start(u) >= x0 ? 0 : 1;
+    const float* w = p.sk_ws + ((u * 2 + slot) * TMW * TN * 512 + threadIdx.x) * 4;
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) acc[tm][tn] += *reinterpret_cast<const f32x4*>(w + (int64_t)(tm * TN + tn) * 512 * 4);
+  }
+  int64_t m0, n0;
+  tile_origin<BM2, BN>(p, p.sk_dp + (int)blockIdx.x, m0, n0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 2, wn = wave & 3;
+#pragma unroll
+  for (int tm = 0; tm < TMW; ++tm) {
+    const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4);
   }
 }
 
@@ -1142,6 +1259,47 @@ int launch(const GemmArgs& p, hipStream_t s) {
   return cullavo_check_launch("gemm");
 }
 
+// ---- stream-K tail ---------------------------------------------------------------------------
+// The 8-wave kernels run one block per CU, so a grid of 1376 tiles takes 6 rounds of 256 for
+// 5.375 rounds of work. With a partial last round, the last full round plus the remainder are
+// given to 256 blocks as equal shares of their K-iterations (each block: whole tiles where its
+// share covers them, f32 partial sums for the at most two tiles it shares), and a fix-up
+// kernel adds each shared tile's partials in K order and runs the epilogue. Auto mode uses it
+// when the last round would leave at least g_sk_min_idle of the CUs idle: the partial sums'
+// round trip through HBM has to be paid for. Off by default: measured on the 7B step's shapes
+// (tools/streamk_bench.py, profiles/r02/streamk_bench.log) it loses 5-43 % -- the partials'
+// write + fix-up read (~0.6 of a round at K = 4096) eat the recovered tail, and the stream-K
+// kernel's piece loop pushes the dW variant past 256 VGPRs (spills).
+int g_streamk = 0;             // 0 off, 1 auto, 2 whenever the last round is partial
+double g_sk_min_idle = 0.25;
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    n = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n;
+}
+
+// one scratch buffer per (device, stream), allocated once at the largest size any 8-wave
+// launch can ask for (2 partial tiles of 256x256 f32 per CU); launches on one stream are
+// ordered, so they can share it
+float* sk_workspace(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, void*> pool;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = pool.find({dev, s});
+  if (it != pool.end()) return (float*)it->second;
+  void* ptr = nullptr;
+  if (hipMalloc(&ptr, (size_t)num_cus() * 2 * 256 * 256 * 4) != hipSuccess) ptr = nullptr;
+  pool[{dev, s}] = ptr;
+  return (float*)ptr;
+}
+
 template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0>
 int launch256(GemmArgs p, hipStream_t s) {
   const int smem = 2 * (BM2 * BK * 2 + BN2 * BK * 2);
@@ -1153,7 +1311,36 @@ int launch256(GemmArgs p, hipStream_t s) {
   }
   p.tiles_m = (int)cdiv(p.M, BM2);
   p.tiles_n = (int)cdiv(p.N, BN2);
-  gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nk = cdiv(p.K, BK);
+  const int slots = num_cus();
+  const int64_t full = tiles / slots, rem = tiles % slots;
+  p.sk_dp = (int)tiles;
+  p.sk_units = 0;
+  p.sk_iters = 0;
+  p.sk_ws = nullptr;
+  const bool want = g_streamk != 0 && rem != 0 && nk >= 4 &&
+                    (g_streamk == 2 || (double)(slots - rem) / slots >= g_sk_min_idle);
+  if (want) {
+    float* ws = sk_workspace(s);
+    if (ws != nullptr) {
+      const int64_t dp = full >= 1 ? (full - 1) * slots : 0;
+      p.sk_dp = (int)dp;
+      p.sk_iters = (tiles - dp) * nk;
+      p.sk_units = (int)std::min<int64_t>(slots, p.sk_iters);
+      p.sk_ws = ws;
+    }
+  }
+  if (p.sk_dp > 0) gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<p.sk_dp, 512, smem, s>>>(p);
+  if (p.sk_units > 0) {
+    static bool sk_attr = false;
+    if (!sk_attr) {
+      (void)hipFuncSetAttribute((const void*)gemm256_sk_k<AL, BL, CT, BM2, BN2, LDR>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+      sk_attr = true;
+    }
+    gemm256_sk_k<AL, BL, CT, BM2, BN2, LDR><<<p.sk_units, 512, smem, s>>>(p);
+    gemm_sk_fixup_k<CT, BM2, BN2><<<(unsigned)(tiles - p.sk_dp), 512, 0, s>>>(p);
+  }
   return cullavo_check_launch("gemm256");
 }
 
@@ -1213,6 +1400,12 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 static int g_force_tile = -1;
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
+
+extern "C" int cullavo_gemm_set_streamk(int mode) {
+  const int prev = g_streamk;
+  if (mode >= 0 && mode <= 2) g_streamk = mode;
+  return prev;
+}
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
@@ -1280,6 +1473,10 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.drop_seed = d.drop_seed;
   p.part = nullptr;
   p.kt_per = 0;
+  p.sk_dp = 0;
+  p.sk_units = 0;
+  p.sk_iters = 0;
+  p.sk_ws = nullptr;
   {
     auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     p.epi_lds = a16(d.C) && a16(d.bias) && a16(d.preact) && a16(residual) && a16(d.addend) &&

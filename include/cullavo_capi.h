@@ -120,6 +120,13 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
+/* Stream-K tail of the 8-wave kernels: 0 = off (default; slower on every 7B step shape
+   measured), 1 = auto (when a partial last round of tiles would leave >= 25 % of the CUs
+   idle), 2 = whenever the last round is partial. The
+   tail's f32 partial sums go to a library-owned scratch buffer, one per (device, stream)
+   (2 x 256x256 f32 per CU, allocated at first use); a fix-up kernel adds them in K order.
+   Returns the previous mode. For tests and tuning; not thread-safe. */
+int cullavo_gemm_set_streamk(int mode);
 /* Tuning/A-B switch. Bit 0: 1 (default) = the 8-wave kernels stage their epilogue through LDS
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
    Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */

@@ -114,6 +114,59 @@ def test_gemm_epilogue_paths_bit_identical(tile_mode):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("M,N,K,al,bl", [(2304, 8192, 1024, 0, 0), (1032, 2056, 4104, 1, 1), (2000, 1544, 520, 0, 1),
+                                          (264, 520, 8704, 1, 1), (1000, 4104, 1032, 0, 0)])
+def test_gemm_streamk_tail(M, N, K, al, bl):
+    """The stream-K tail of the 8-wave kernels (cullavo_gemm_set_streamk 2: every launch whose last
+    round of tiles is partial) against the fp32 product and the data-parallel launch; the K split
+    and the partials' order are fixed, so two runs are bitwise equal; ragged tiles, a grid smaller
+    than the CU count (many blocks per tile) and K not a multiple of the K-tile included."""
+    from cullavo_amd import _lib
+    A = rnd((M, K), 41)
+    B = rnd((N, K), 42)
+    ref = A.float() @ B.float().T
+    Ad = (A if al == 0 else A.T.contiguous()).to(DEV)
+    Bd = (B if bl == 0 else B.T.contiguous()).to(DEV)
+    outs = {}
+    prev = _lib.lib().cullavo_gemm_set_streamk(0)
+    try:
+        for mode in (0, 2, 2):
+            _lib.lib().cullavo_gemm_set_streamk(mode)
+            C = torch.full((M, N), float("nan"), dtype=BF, device=DEV)
+            ops().gemm(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), C, N)
+            outs.setdefault(mode, []).append(C)
+    finally:
+        _lib.lib().cullavo_gemm_set_streamk(prev)
+    close(outs[2][0], ref, 8e-3, f"stream-K {al}{bl} {M}x{N}x{K}")
+    close(outs[2][0], outs[0][0].float(), 8e-3, "stream-K vs data-parallel")
+    assert torch.equal(outs[2][0], outs[2][1]), "stream-K not reproducible"
+
+
+def test_gemm_streamk_epilogues():
+    """Stream-K fix-up runs the full epilogue: bias, GELU, residual, preact, bf16 accumulate and
+    the f32 beta=1 weight-gradient path, equal to the data-parallel launch within bf16 rounding."""
+    from cullavo_amd import _lib
+    M, N, K = 1288, 2312, 1040
+    x, w, b = rnd((M, K), 51).to(DEV), rnd((N, K), 52, 0.1).to(DEV), rnd((N,), 53, 0.1).to(DEV)
+    r = rnd((M, N), 54).to(DEV)
+    dy = rnd((M, N), 55).to(DEV)
+    res = {}
+    prev = _lib.lib().cullavo_gemm_set_streamk(0)
+    try:
+        for mode in (0, 2):
+            _lib.lib().cullavo_gemm_set_streamk(mode)
+            y, pre = ops().linear(x, w, b, act=ops().ACT_GELU, residual=r, want_preact=True)
+            acc = rnd((N, K), 56, dtype=torch.float32).to(DEV)
+            ops().linear_dw(dy, x, acc, beta=1.0)
+            accb = rnd((N, K), 57).to(DEV)
+            ops().linear_dw(dy, x, accb, beta=1.0)
+            res[mode] = (y, pre, acc, accb)
+    finally:
+        _lib.lib().cullavo_gemm_set_streamk(prev)
+    for name, a, c in zip(("y", "preact", "dw f32", "dw bf16"), res[0], res[2]):
+        close(c, a.float(), 8e-3 if a.dtype == BF else 1e-5, f"stream-K {name}")
+
+
 def test_gemm_f32_accumulate_beta(tile_mode):
     M, N, K = 128, 192, 256
     dy, x = rnd((M, N), 7), rnd((M, K), 8)
