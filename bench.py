@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the optimizer update in-stream instead of under the next forward (A/B)")
     ap.add_argument("--workload", default="step", choices=["step", "vit"],
                     help="step: the training step (default; configs 3/4/5 by --config/--batch/--text-len); "
                          "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64)")
@@ -310,7 +312,7 @@ def main():
     opt = {"MODEL": {"CONFIG": args.config}, "LLM": {"TRAINABLE": args.trainable},
            "DATA": {"BATCH_SIZE_PER_GPU": args.batch, "TEXT_LEN": args.text_len, "IMAGE_COL": 35,
                     "STEPS": args.warmup + args.steps},
-           "BUCKET_MB": args.bucket_mb}
+           "BUCKET_MB": args.bucket_mb, "OPTIMIZER": {"OVERLAP": not args.no_overlap}}
     tr = CuLLaVO_Trainer(opt)
     rank = tr.accel.process_index
     tr.init_train()

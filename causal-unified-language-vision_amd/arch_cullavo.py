@@ -195,8 +195,12 @@ class CuLLaVOModel(nn.Module):
                 raise ValueError(f"Expected input batch_size ({B * (L - 1)}) to match target batch_size "
                                  f"({labels.shape[0] * (labels.shape[-1] - 1)}).")
             targets = ops.shift_targets(labels, attention_mask, cfg.ignore_index)
+            for ar in self.arenas.values():  # final norm / lm_head: pending optimizer updates
+                ar.wait_update()
             loss, logits = HeadLossFn.apply(h, lm, targets, cfg.ignore_index, *lm.head_params())
         else:
+            for ar in self.arenas.values():
+                ar.wait_update()
             logits = lm.lm_head(lm.model.norm(h))
         logits = logits.view(B, L, -1)
         hs_t = tuple(t.view(B, L, d) for t in hs) if hs else None
@@ -244,6 +248,8 @@ class CuLLaVOModel(nn.Module):
         from .generation import sample_next
         if not use_cache:
             raise NotImplementedError("generate() runs on the KV cache (use_cache=True)")
+        for ar in self.arenas.values():  # pending optimizer updates (FusedAdamW overlap)
+            ar.wait_update()
         cfg = self.config
         pad = pad_token_id if pad_token_id is not None else cfg.pad_token_id
         B, S = input_ids.shape

@@ -46,6 +46,10 @@ class ParamArena:
         self._write_hooks: list = []  # called with the keys whose gradient write is enqueued
         self._writes = 0  # writes torch's version counter cannot see (kernels on raw pointers)
         self._kmajor: dict[str, list] = {}  # first_key -> [buffer [K, N], state made from, pending event]
+        # (lo, hi, event): parameter updates of elements [lo, hi) still running on the
+        # optimizer's side stream (FusedAdamW(overlap=True)); consumers call wait_update
+        self._pending: list = []
+        self._spans: dict[str, tuple[int, int]] = {}
         if trainable:
             self.grad_flat = torch.zeros(off, dtype=dtype, device=self.device)
             self._attach_grads()
@@ -115,6 +119,32 @@ class ParamArena:
             if self.offsets[b][0] != oa + na:
                 raise RuntimeError(f"arena {self.name}: {a} and {b} are not adjacent")
 
+    def span(self, prefix: str) -> tuple[int, int]:
+        """element range [lo, hi) of the keys starting with prefix (one layer's parameters)"""
+        sp = self._spans.get(prefix)
+        if sp is None:
+            sp = self._spans[prefix] = self.slice_of([k for k in self.offsets if k.startswith(prefix)])
+        return sp
+
+    # -- deferred optimizer updates ------------------------------------------------------------
+    def defer(self, lo: int, hi: int, event):
+        self._pending.append((lo, hi, event))
+
+    def wait_update(self, lo: int | None = None, hi: int | None = None):
+        """Make the current stream wait for the pending side-stream updates of elements [lo, hi)
+        (all of them when lo is None). Forward consumers call it per layer, so the next step's
+        forward overlaps the optimizer update of the layers it has not reached yet."""
+        if not self._pending:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        keep = []
+        for a, b, ev in self._pending:
+            if lo is None or (a < hi and lo < b):
+                cur.wait_event(ev)
+            else:
+                keep.append((a, b, ev))
+        self._pending = keep
+
     def slice_of(self, keys: list[str]) -> tuple[int, int]:
         lo = min(self.offsets[k][0] for k in keys)
         hi = max(self.offsets[k][0] + self.offsets[k][1] for k in keys)
@@ -130,6 +160,7 @@ class ParamArena:
         cycle, 1 afterwards. `span` widens the view over adjacent keys (fused weights)."""
         if not self.trainable:
             raise RuntimeError(f"arena {self.name} is frozen")
+        self.wait_update()  # the optimizer's side stream may still read last step's gradients
         if self.params[key].grad is None:  # e.g. optimizer.zero_grad(set_to_none=True)
             self._attach_grads()
         beta = 1.0 if key in self._written else 0.0
@@ -153,6 +184,8 @@ class ParamArena:
         uses beta = 0. Parameters that were never written last cycle are zeroed explicitly."""
         if self.trainable:
             unwritten = [k for k in self.offsets if k not in self._written]
+            if unwritten:
+                self.wait_update()  # a side-stream optimizer update may still read these gradients
             for k in unwritten:
                 o, n, _ = self.offsets[k]
                 self.grad_flat[o:o + n].zero_()

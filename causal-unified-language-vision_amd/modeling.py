@@ -33,6 +33,17 @@ if KMAJOR_MODE not in ("side", "sync", "off"):
 _SIDE: dict = {}
 
 
+def _wait_updates(arena, prefix, lora_groups):
+    """The current stream waits for the optimizer's pending side-stream update of this layer's
+    parameters (and of the LoRA arena) -- no-op unless FusedAdamW(overlap=True) left one."""
+    arena.wait_update(*arena.span(prefix))
+    for g in lora_groups.values():
+        la = getattr(g, "arena", None)
+        if la is not None:
+            la.wait_update()
+            break
+
+
 def _side_stream(device):
     key = torch.device(device)
     if key not in _SIDE:
@@ -229,6 +240,7 @@ class CLIPEncoderLayer(nn.Module):
         return [p for p in self.parameters() if p.requires_grad]
 
     def run(self, h2d, B, T, lora_seed: int = 0):
+        _wait_updates(self._arena, self._lp, self.lora_groups)
         return ClipLayerFn.apply(h2d, self, B, T, lora_seed, *self.fn_params())
 
     def forward(self, hidden_states, attention_mask=None, causal_attention_mask=None, **kw):
@@ -345,6 +357,9 @@ class LlavaMultiModalProjector(nn.Module):
         x = image_features.reshape(-1, shp[-1])
         if not x.is_contiguous():
             x = x.contiguous()
+        for p in self.parameters():
+            p._cv_arena.wait_update()  # a pending optimizer update (FusedAdamW overlap)
+            break
         y = ProjectorFn.apply(x, self, *self.fn_params())
         return y.view(*shp[:-1], y.shape[-1])
 
@@ -416,6 +431,7 @@ class LlamaDecoderLayer(nn.Module):
         return [p for p in self.parameters() if p.requires_grad]
 
     def run(self, h2d, sctx: StepContext):
+        _wait_updates(self._arena, self._lp, self.lora_groups)
         if torch.is_grad_enabled() and h2d.requires_grad:
             self.prefetch_kmajor()
         return LlamaLayerFn.apply(h2d, self, sctx, *self.fn_params())
@@ -447,6 +463,7 @@ class _Embedding(nn.Module):
         return self.weight.shape[1]
 
     def forward(self, ids):
+        self.weight._cv_arena.wait_update()  # a pending optimizer update (FusedAdamW overlap)
         return EmbeddingFn.apply(ids.contiguous(), self.weight)
 
 

@@ -155,6 +155,8 @@ class BaseModel(nn.Module):
     def save_pretrained(self, save_dir, epoch, accel):
         """reference modeling/BaseModel.py:20-69 (checkpoint.save_cullavo)"""
         from .checkpoint import save_cullavo
+        for ar in self.cullavo_model.arenas.values():  # pending optimizer updates (FusedAdamW overlap)
+            ar.wait_update()
         save_cullavo(self.cullavo_model, save_dir, epoch, is_main_process=accel.is_main_process)
         import torch.distributed as dist
         if dist.is_initialized() and dist.get_world_size() > 1:

@@ -163,6 +163,7 @@ class DefaultTrainer:
                 with self.accel.accumulate(self.model):
                     info, _, _ = self.train_step(batch)
                 losses.append(info["loss_llm"])
+        self.optimizer.synchronize()
         return losses
 
 
@@ -171,7 +172,9 @@ class CuLLaVO_Trainer(DefaultTrainer):
         """reference trainer/cullavo_trainer.py:12-14: AdamW(lr, wd) + CosineAnnealingLR."""
         o = self.opt["OPTIMIZER"]
         cm = self.model.cullavo_model if hasattr(self.model, "cullavo_model") else self.model
-        self.optimizer = FusedAdamW(list(cm.arenas.values()), lr=float(o["LR"]), weight_decay=float(o["WEIGHT_DECAY"]))
+        # OVERLAP: the update runs on a side stream under the next step's forward (optim.py)
+        self.optimizer = FusedAdamW(list(cm.arenas.values()), lr=float(o["LR"]), weight_decay=float(o["WEIGHT_DECAY"]),
+                                    overlap=bool(o.get("OVERLAP", True)))
         self.lr_scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(
             optimizer=self.optimizer, T_max=max(1, len(self.train_dataloaders) * int(o["EPOCH"])),
             eta_min=float(o["LAST_LR"]))

@@ -188,6 +188,31 @@ def test_dw_side_stream_bitwise(monkeypatch):
         assert torch.equal(a, b), i
 
 
+def test_adamw_overlap_bitwise():
+    """FusedAdamW(overlap=True): the update runs on a side stream per decoder layer and the next
+    forward waits per layer; parameters, moments and losses over three steps are bitwise equal to
+    the in-stream update (synchronize() before reading parameters outside a forward)."""
+    from cullavo_amd.optim import FusedAdamW
+    ids, mask, pix, labels = inputs()
+    res = {}
+    for overlap in (False, True):
+        m = build()
+        opt = FusedAdamW(list(m.arenas.values()), lr=1e-3, overlap=overlap)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
+            out.loss.backward()
+            opt.clip_grad_norm_(1.0)
+            opt.step()
+            losses.append(out.loss.detach().clone())
+        opt.synchronize()
+        res[overlap] = (torch.stack(losses), torch.cat([a.flat.float() for a in m.arenas.values()]),
+                        torch.cat([torch.cat([mm.float(), vv.float()]) for mm, vv in opt.flat_state]))
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+
+
 def test_adamw_skips_parameters_without_gradient():
     """A text-only batch never reaches the projector: like torch.optim.AdamW on a parameter
     whose .grad is None, FusedAdamW leaves it (and its step count) untouched, while the
