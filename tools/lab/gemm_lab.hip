@@ -12,7 +12,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr unsigned kOOB = 0x7FFFFFF0u;
 
 enum : int { F_NODMA = 1, F_NOMFMA = 2, F_LDR1 = 4, F_NOEPI = 8, F_SPLITKS = 16, F_STAG = 32, F_SPLIT2 = 64,
-             F_NOWAIT = 128, F_NOBAR = 256, F_SPREAD = 512 };
+             F_NOWAIT = 128, F_NOBAR = 256, F_SPREAD = 512, F_REGS = 1024, F_MIDW = 2048 };
 
 DEV int img0_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
@@ -57,6 +57,31 @@ DEV frag8 read_frag0(const char* lds, int rbase, int ks, int lane) {
   const int c = ks * 4 + (lane >> 4);
   u16x8 v = *reinterpret_cast<const u16x8*>(lds + img0_off(row, c));
   return __builtin_bit_cast(frag8, v);
+}
+
+// register staging (F_REGS): the next K-tile is read by plain 16-B buffer loads into VGPRs
+// (8 threads per 128-B row segment, coalesced) and written to the same swizzled image with
+// ds_write_b128, instead of LDS-DMA pieces
+template <int ROWS>
+DEV void regs_load0(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
+                    u16x8 (&r)[ROWS / 64]) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 64; ++i) {
+    const int q = threadIdx.x + 512 * i;
+    const int row = q >> 3, c = q & 7;
+    const int64_t gi = idx0 + row, gk = k0 + c * 8;
+    const unsigned off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
+    r[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+  }
+}
+template <int ROWS>
+DEV void regs_store0(char* lds, const u16x8 (&r)[ROWS / 64]) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 64; ++i) {
+    const int q = threadIdx.x + 512 * i;
+    const int row = q >> 3, c = q & 7;
+    *reinterpret_cast<u16x8*>(lds + img0_off(row, c)) = r[i];
+  }
 }
 
 struct LabArgs {
@@ -168,6 +193,7 @@ __global__ __launch_bounds__(512, 1) void lab256_k(LabArgs p) {
           if (wave < 4) dma_tile0<BM2, 4>(ra, p.K, m0, p.M, k1, p.K, nxt, wave, lane);
         }
       }
+    } else if constexpr (FL & F_REGS) {
     } else if (more && !(FL & F_NODMA) && !(FL & F_SPREAD)) {
       if constexpr (FL & F_LDR1) {
         if (wave < 4) {
@@ -179,8 +205,21 @@ __global__ __launch_bounds__(512, 1) void lab256_k(LabArgs p) {
         dma_tile0<BN, 8>(rb, p.K, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
       }
     }
+    u16x8 rga[BM2 / 64], rgb[BN / 64];
+    if constexpr (FL & F_REGS) {
+      if (more) {
+        regs_load0<BM2>(ra, p.K, m0, p.M, k1, p.K, rga);
+        regs_load0<BN>(rb, p.K, n0, p.N, k1, p.K, rgb);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if constexpr ((FL & F_REGS) && (FL & F_MIDW)) {
+        if (ks == 1 && more) {
+          regs_store0<BM2>(nxt, rga);
+          regs_store0<BN>(nxt + TILE_A, rgb);
+        }
+      }
       if constexpr (FL & (F_STAG | F_SPLIT2)) {
         if (ks == 1 && more) {
           if constexpr (FL & F_STAG) {
@@ -223,7 +262,13 @@ __global__ __launch_bounds__(512, 1) void lab256_k(LabArgs p) {
         for (int t = 0; t < TN; ++t) asm volatile("" ::"v"(fb[t]));
       }
     }
-    if constexpr (!(FL & F_NOWAIT)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr ((FL & F_REGS) && !(FL & F_MIDW)) {
+      if (more) {
+        regs_store0<BM2>(nxt, rga);
+        regs_store0<BN>(nxt + TILE_A, rgb);
+      }
+    }
+    if constexpr (!(FL & F_NOWAIT) && !(FL & F_REGS)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!(FL & F_NOBAR)) __syncthreads();
   }
 
@@ -914,7 +959,7 @@ extern "C" int lab_gemm(int variant, int64_t M, int64_t N, int64_t K, const void
     V(256, 0) V(256, 1) V(256, 2) V(256, 3) V(256, 4) V(256, 5) V(256, 8) V(256, 9) V(256, 10) V(256, 12)
     V(256, 16) V(256, 20) V(256, 17) V(256, 48) V(256, 80) V(192, 48) V(192, 80)
     V(192, 0) V(192, 1) V(192, 2) V(192, 4) V(192, 8) V(192, 16) V(192, 20)
-    V(256, 128) V(256, 384) V(256, 257) V(256, 144) V(256, 528) V(256, 656) V(256, 912)
+    V(256, 1040) V(256, 3088) V(192, 1040) V(192, 3088) V(256, 1024) V(256, 128) V(256, 384) V(256, 257) V(256, 144) V(256, 528) V(256, 656) V(256, 912)
 #undef V
     case 400: return launch4<0>(p, s);
     case 401: return launch4<1>(p, s);
