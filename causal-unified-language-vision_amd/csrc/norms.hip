@@ -222,6 +222,130 @@ __global__ __launch_bounds__(512, WANT_DW ? 2 : 4) void rmsnorm_bwd8_k(const T* 
   }
 }
 
+// Pipelined form (the default with dw since round 2): one 8-wave workgroup per CU, two register sets,
+// so the next rows' x / dy / dres loads are in flight while the current rows run their two
+// passes, the dot-product barrier and their stores (rmsnorm_bwd8_k drains the loads at every
+// iteration). Four waves per row (wave part p owns the 512-column chunks p, p+4, ...), two rows
+// per iteration, so two register sets fit without spilling at 4096 columns. Per-element
+// arithmetic is rmsnorm_bwd8_k's; the row's dot product adds its four wave partials in order
+// (dx differs from rmsnorm_bwd8_k only in that sum's order); dw folds 256 partial rows in a fixed
+// order (deterministic).
+constexpr int kBwd8pBlocks = 256;
+constexpr int kWpr = 4;             // waves per row
+constexpr int kSlots = 8 / kWpr;    // rows per iteration
+
+template <typename T, int NH, bool HAS_DRES>
+struct BwdRows {
+  Raw8<T> xr[NH], dr[NH], rr[NH];
+  float r;
+  DEV void load(const T* x, const T* dy, const T* dres, const float* rstd, int64_t row, bool live, int part,
+                int lane, int nch, int cols) {
+    r = live ? rstd[row] : 0.f;
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (kWpr * c + part) * 512 + lane * 8;
+      if (live && kWpr * c + part < nch && col < cols) {
+        xr[c].load(x + row * cols + col);
+        dr[c].load(dy + row * cols + col);
+        if (HAS_DRES) rr[c].load(dres + row * cols + col);
+      }
+    }
+  }
+};
+
+template <typename T, int NCH, bool WANT_DW, bool HAS_DRES>
+__global__ __launch_bounds__(512, 1) void rmsnorm_bwd8p_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ w, const float* __restrict__ rstd,
+                                                          T* __restrict__ dx, const T* __restrict__ dres,
+                                                          float* __restrict__ part, int64_t rows, int cols,
+                                                          int64_t rows_per_block) {
+  constexpr int NH = (NCH + kWpr - 1) / kWpr;
+  extern __shared__ float sdw[];
+  __shared__ float pdot[2][kSlots][kWpr];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = wave / kWpr, wp = wave % kWpr;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float acc[NH][8];
+#pragma unroll
+  for (int c = 0; c < NH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  const int iters = (int)cdiv(max(r1 - r0, (int64_t)0), (int64_t)kSlots);
+
+  auto body = [&](const BwdRows<T, NH, HAS_DRES>& cur, int it) {
+    const int64_t row = r0 + kSlots * it + slot;
+    const bool live = row < r1;
+    const float r = cur.r;
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (kWpr * c + wp) * 512 + lane * 8;
+      if (live && kWpr * c + wp < NCH && col < cols) {
+        Raw8<T> wr;
+        wr.load(w + col);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = cur.xr[c][j] * r;
+          dot += cur.dr[c][j] * wr[j] * xh;
+          if (WANT_DW) acc[c][j] += cur.dr[c][j] * Elt<T>::rnd(xh);
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) pdot[it & 1][slot][wp] = dot;
+    __syncthreads();
+    dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kWpr; ++i) dot += pdot[it & 1][slot][i];
+    dot /= (float)cols;
+#pragma unroll
+    for (int c = 0; c < NH; ++c) {
+      const int col = (kWpr * c + wp) * 512 + lane * 8;
+      if (live && kWpr * c + wp < NCH && col < cols) {
+        Raw8<T> wr;
+        wr.load(w + col);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = r * (cur.dr[c][j] * wr[j] - cur.xr[c][j] * r * dot);
+          if (HAS_DRES) o[j] += cur.rr[c][j];
+        }
+        store8(dx + row * cols + col, o);
+      }
+    }
+  };
+  auto load = [&](BwdRows<T, NH, HAS_DRES>& dst, int it) {
+    const int64_t row = r0 + kSlots * it + slot;
+    dst.load(x, dy, dres, rstd, row, it < iters && row < r1, wp, lane, NCH, cols);
+  };
+
+  BwdRows<T, NH, HAS_DRES> ra, rb;
+  load(ra, 0);
+  for (int it = 0; it < iters; it += 2) {
+    load(rb, it + 1);  // rows of the next iteration in flight under this one
+    body(ra, it);
+    if (it + 1 >= iters) break;
+    load(ra, it + 2);
+    body(rb, it + 1);
+  }
+  if (WANT_DW) {  // fold the row slots in order; the parts of a row own disjoint columns
+    for (int sl = 0; sl < kSlots; ++sl) {
+      if (slot == sl) {
+#pragma unroll
+        for (int c = 0; c < NH; ++c) {
+          const int col = (kWpr * c + wp) * 512 + lane * 8;
+          if (kWpr * c + wp < NCH && col < cols)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sdw[col + j] = (sl == 0 ? 0.f : sdw[col + j]) + acc[c][j];
+        }
+      }
+      __syncthreads();
+    }
+    for (int col = threadIdx.x; col < cols; col += 512) part[(int64_t)blockIdx.x * cols + col] = sdw[col];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 template <typename T, int NCH>
 __global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -421,6 +545,14 @@ extern "C" int cullavo_rmsnorm_fwd(const void* x, const void* w, void* y, float*
   return cullavo_check_launch("rmsnorm_fwd");
 }
 
+static int g_rms_bwd_mode = 1;  // 1 = pipelined 8-wave kernel (default), 0 = rmsnorm_bwd8_k
+
+extern "C" int cullavo_rmsnorm_set_bwd(int mode) {
+  const int prev = g_rms_bwd_mode;
+  if (mode == 0 || mode == 1) g_rms_bwd_mode = mode;
+  return prev;
+}
+
 extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd,
                                    void* dx, const void* dres, void* dw, int w_dtype, float beta, float* ws,
                                    int64_t rows, int64_t cols, int dtype, void* stream) {
@@ -431,11 +563,15 @@ extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w,
   const int nch = nch_for(cols);
   const bool want = dw != nullptr, hr = dres != nullptr;
   const bool wide = nch > 8;  // 8192 columns: the 4-wave kernel (register budget)
-  const int nb = wide ? bwd_blocks(rows) : (int)std::min<int64_t>(kBwd8Blocks, cdiv(rows, 4));
+  // the pipelined kernel only pays when dw is wanted (measured, tools/norm_bench.py: without dw the
+  // round-1 kernel's four waves per SIMD already stream at ~5.8 TB/s)
+  const bool pipe = !wide && want && g_rms_bwd_mode == 1;
+  const int nb = wide ? bwd_blocks(rows) : (int)std::min<int64_t>(pipe ? kBwd8pBlocks : kBwd8Blocks, cdiv(rows, 4));
   const int64_t rpb = cdiv(rows, nb);
   const size_t lds = want ? (size_t)cols * sizeof(float) : 0;
 #define RMB(T, WD, HR)                                                                                        \
   if (wide) rmsnorm_bwd_k<T, 16, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols); \
+  else if (pipe) NCH_DISPATCH(nch, rmsnorm_bwd8p_k<T, (NC > 8 ? 8 : NC), WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb)) \
   else NCH_DISPATCH(nch, rmsnorm_bwd8_k<T, (NC > 8 ? 8 : NC), WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb))
   if (dtype == CULLAVO_DT_BF16) {
     if (want && hr) { RMB(u16, true, true); } else if (want) { RMB(u16, true, false); }

@@ -144,6 +144,11 @@ int cullavo_rmsnorm_fwd(const void* x, const void* w, void* y, float* rstd, int6
 int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
                         const void* dres, void* dw, int w_dtype, float beta, float* workspace,
                         int64_t rows, int64_t cols, int dtype, void* stream);
+/* A/B switch for the bf16/f32 RMSNorm backward with dw at <= 4096 columns: 1 (default) = the
+   pipelined one-workgroup-per-CU kernel (next rows' loads in flight under the current rows), 0 = the
+   round-1 kernel (two waves per row). Both are deterministic; they add a row's dot-product
+   partials and dw's partial rows in different fixed orders. Returns the previous mode. */
+int cullavo_rmsnorm_set_bwd(int mode);
 /* nn.LayerNorm (CLIP pre_layrnorm / layer_norm1/2, tf:clip/modeling_clip.py:353-384,642).
  * mean/rstd: [rows] f32 saved for backward. The backwards add an optional residual-stream
  * gradient dres (nullable) into dx, fusing the residual branch join. */

@@ -242,6 +242,37 @@ def test_rmsnorm(rows, cols):
     close(dw, wr.grad, 1e-2, "rms dw")
 
 
+@pytest.mark.parametrize("rows,cols", [(8704, 4096), (1037, 4096), (3, 4096), (515, 1024)])
+def test_rmsnorm_bwd_modes(rows, cols):
+    """Pipelined backward (mode 1, default) vs the round-1 kernel (mode 0) and the oracle, at the
+    config-3 shape and ragged row counts (partial last iterations / empty workgroups)."""
+    from cullavo_amd import _lib
+    x, w = rnd((rows, cols), 40), (1 + 0.1 * rnd((cols,), 41).float()).to(BF)
+    dy, dres = rnd((rows, cols), 42), rnd((rows, cols), 43)
+    _, rstd = ops().rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5)
+    L = _lib.lib()
+    outs = {}
+    try:
+        for mode in (0, 1):
+            L.cullavo_rmsnorm_set_bwd(mode)
+            dw = torch.empty(cols, dtype=torch.float32, device=DEV)
+            dx = ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV), dw=dw)
+            dx2 = ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV), dw=dw)
+            assert torch.equal(dx, dx2), "rmsnorm_bwd is not deterministic"
+            outs[mode] = (dx.float(), dw.clone())
+    finally:
+        L.cullavo_rmsnorm_set_bwd(1)
+    (dx0, dw0), (dx1, dw1) = outs[0], outs[1]
+    # same per-element arithmetic; only the row dot product's partial-sum order differs
+    assert (dx1 - dx0).abs().max().item() <= 2 * (dx0.abs().max().item() * 2 ** -7)
+    assert ((dw1 - dw0).norm() / dw0.norm()).item() < 1e-5
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    O.rmsnorm(xr, wr, 1e-5).backward(dy.float())
+    close(dx1, xr.grad + dres.float(), 1e-2, "rms dx (pipelined)")
+    close(dw1, wr.grad, 1e-2, "rms dw (pipelined)")
+
+
 @pytest.mark.parametrize("rows,cols", [(64, 1024), (577, 128), (3, 64)])
 def test_layernorm(rows, cols):
     x = rnd((rows, cols), 30, 2.0)
