@@ -231,6 +231,11 @@ size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
    in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */
 int cullavo_attn_set_bwd_tiles(int mode);
+/* A/B switch for the attention forward's K/V tile staging: 1 (default) = 16-B buffer loads
+   whose range check zero-fills rows past the sequence end, 0 = pointer loads behind a per-chunk
+   bounds branch. Results are identical. Synchronous (device symbol copy); returns the previous
+   setting, -1 on a HIP error. */
+int cullavo_attn_set_stage(int buffer_loads);
 
 /* ---- KV-cache decode (generate) --------------------------------------
  * Cache per layer: K, V [B, Lmax, H*D] bf16, token stride ld_tok, batch stride ld_batch.

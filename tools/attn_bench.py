@@ -22,7 +22,13 @@ def timeit(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
-for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("ViT D64", 64, 577, 16, 64, False)]:
+STAGES = [int(x) for x in os.environ.get("ATTN_STAGE_AB", "1").split(",")]  # e.g. 1,0,1,0
+ref_out = {}
+for stage in STAGES:
+  if len(STAGES) > 1:
+    _lib.lib().cullavo_attn_set_stage(stage)
+  for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("ViT D64", 64, 577, 16, 64, False)]:
+    torch.manual_seed(0)
     qkv = (torch.randn(B * L, 3 * H * D, device="cuda") * 0.5).bfloat16()
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     o, lse = ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal)
@@ -41,5 +47,12 @@ for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("V
         res.append(f"m{mode} {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.1f} TF")
     diff = ((outs[4] - outs[1]).norm() / outs[1].norm()).item()
     res.append(f"rel(m4, m1) {diff:.1e} rel(m7, m1) {((outs[7] - outs[1]).norm() / outs[1].norm()).item():.1e}")
+    key = name
+    cur = (o.float().clone(), outs[7])
+    if key in ref_out:
+        res.append(f"bitwise equal across staging: {torch.equal(ref_out[key][0], cur[0]) and torch.equal(ref_out[key][1], cur[1])}")
+    else:
+        ref_out[key] = cur
     _lib.lib().cullavo_attn_set_bwd_tiles(-1)
-    print(f"{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd " + " | ".join(res))
+    tag = f"stage {stage} " if len(STAGES) > 1 else ""
+    print(f"{tag}{name:16s} fwd {tf * 1e3:8.1f} us {fl / tf / 1e9:7.1f} TF | bwd " + " | ".join(res), flush=True)
