@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--high-prio", action="store_true",
+                    help="run the training step on a high-priority HIP stream (the optimizer's side stream "
+                         "stays at the default priority; A/B experiment)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the optimizer update in-stream instead of under the next forward (A/B)")
     ap.add_argument("--workload", default="step", choices=["step", "vit"],
@@ -319,7 +322,16 @@ def main():
     cm = tr.model.cullavo_model
     batch = next(iter(tr.train_dataloaders))  # resident in HBM before timing
 
+    prio_stream = None
+    if args.high_prio:
+        prio_stream = torch.cuda.Stream(priority=-1)
+        prio_stream.wait_stream(torch.cuda.current_stream())
+
     def step():
+        if prio_stream is not None:
+            with torch.cuda.stream(prio_stream), tr.accel.accumulate(tr.model):
+                info, _, _ = tr.train_step(batch)
+            return info["loss_llm"]
         with tr.accel.accumulate(tr.model):
             info, _, _ = tr.train_step(batch)
         return info["loss_llm"]
