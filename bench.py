@@ -63,12 +63,12 @@ def vit_main(args):
     from cullavo_amd.config import CLIPVisionConfig, CuLLaVOConfig
     from cullavo_amd.modeling import CLIPVisionTransformer, clip_specs, init_random_
     from cullavo_amd.perf import flops_per_sample, needed_vision_layers
-    from cullavo_amd.trainer import init_distributed
+    from cullavo_amd.trainer import init_distributed, local_device_index
 
     init_distributed()
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", 0)))
+    torch.cuda.set_device(local_device_index())
     vc = CLIPVisionConfig()
     cfg = CuLLaVOConfig(vision_config=vc)
     ar = ParamArena("vision", clip_specs(vc, "vision_tower.vision_model."), device="cuda")

@@ -49,7 +49,7 @@ class Accel:
         self.num_processes = dist.get_world_size() if self.distributed else 1
         self.process_index = dist.get_rank() if self.distributed else 0
         self.local_process_index = int(os.environ.get("LOCAL_RANK", 0))
-        self.device = torch.device("cuda", self.local_process_index) if torch.cuda.is_available() else \
+        self.device = torch.device("cuda", local_device_index()) if torch.cuda.is_available() else \
             torch.device("cpu")
         self.is_main_process = self.process_index == 0
         self.is_local_main_process = self.local_process_index == 0
@@ -80,13 +80,18 @@ class Accel:
         yield
 
 
+def local_device_index() -> int:
+    """LOCAL_RANK's GPU; more ranks than GPUs (a gloo rehearsal of the DP path on one GPU) share
+    the GPUs round-robin."""
+    return int(os.environ.get("LOCAL_RANK", 0)) % max(torch.cuda.device_count(), 1)
+
+
 def init_distributed(backend: str | None = None):
     """One process per GPU from torchrun's env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_*)."""
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1 and not dist.is_initialized():
-        local = int(os.environ.get("LOCAL_RANK", 0))
         if torch.cuda.is_available():
-            torch.cuda.set_device(local)
-        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+            torch.cuda.set_device(local_device_index())
+        backend = backend or os.environ.get("CULLAVO_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend, timeout=datetime.timedelta(seconds=18000))  # :16 of the ref
 
 
