@@ -168,6 +168,30 @@ DEV float act_apply(int act, float x) {
   return x;
 }
 
+// quick_gelu of act_apply on 8 values, two at a time: the products and the sum as packed f32
+// (v_pk_mul_f32 / v_pk_add_f32) and both bf16 roundings as one v_cvt_pk_bf16_f32 per pair; the
+// same operations in the same order as act_apply, so bit-identical (the epilogue of the ViT fc1
+// GEMM, where the activation was ~30 % of the GEMM's time, tools/vit_gemm_bench.py)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+DEV f32x2v round_bf2(f32x2v x) {
+  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2v));
+  return f32x2v{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+}
+DEV void quick_gelu8(float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f32x2v x = {v[j], v[j + 1]};
+    const f32x2v t = round_bf2(1.702f * x);
+    const f32x2v a = t * -1.4426950408889634f;
+    const f32x2v d = 1.f + f32x2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    const f32x2v sg = round_bf2(f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)});
+    const f32x2v y = sg * x;
+    v[j] = y.x;
+    v[j + 1] = y.y;
+  }
+}
+
 // bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
 DEV int xcd_remap(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -270,8 +294,12 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
       for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
       *reinterpret_cast<u16x8*>(p.preact + m * p.ldc + n) = o;
     }
+    if (p.act == CULLAVO_ACT_QUICK_GELU) {
+      quick_gelu8(v);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
+    }
   }
   if (p.residual) {
     const u16x8 rv = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);

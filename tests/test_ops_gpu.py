@@ -93,18 +93,21 @@ def test_gemm_epilogues(act, tile_mode, epi_mode):
     close(y, a.to(BF).float() + r.float(), 8e-3, "epilogue")
 
 
-def test_gemm_epilogue_paths_bit_identical(tile_mode):
-    """The LDS-staged 16-B epilogue and the per-lane one compute the same roundings in the same
-    order, so every output (bias, LoRA addend, residual, preact, accumulate) is bit-identical."""
+@pytest.mark.parametrize("act", ["gelu", "quick_gelu"])
+def test_gemm_epilogue_paths_bit_identical(tile_mode, act):
+    """The LDS-staged 16-B epilogue (packed quick_gelu) and the per-lane one compute the same
+    roundings in the same order, so every output (bias, LoRA addend, residual, preact, activation,
+    accumulate) is bit-identical."""
     from cullavo_amd import _lib
     M, N, K = 520, 776, 320
     x, w, b = rnd((M, K), 31).to(DEV), rnd((N, K), 32, 0.1).to(DEV), rnd((N,), 33, 0.1).to(DEV)
     r, t = rnd((M, N), 34).to(DEV), rnd((M, N), 35, 0.05).to(DEV)
+    code = ops().ACT_GELU if act == "gelu" else ops().ACT_QUICK_GELU
     outs = []
     for epi in (1, 0):
         prev = _lib.lib().cullavo_gemm_set_epilogue(epi)
         try:
-            y, pre = ops().linear(x, w, b, act=ops().ACT_GELU, residual=r, want_preact=True, addend=t)
+            y, pre = ops().linear(x, w, b, act=code, residual=r, want_preact=True, addend=t)
             acc = rnd((N, K), 36, dtype=torch.float32).to(DEV)
             ops().linear_dw(y, x, acc, beta=1.0)
             outs.append((y, pre, acc))
