@@ -26,9 +26,13 @@ DEV float round_bf(float f) { return bf2f(f2bf(f)); }
 
 // ---- LoRA dropout mask ------------------------------------------------------------------------
 // Counter-based, so the forward (operand staging), dA (operand staging) and dX (GEMM epilogue)
-// regenerate the same mask from (seed, token, feature) without storing it. Element kept iff
-// (hash >> 8) >= thr24 = round(p * 2^24); kept values are scaled by 1/(1-p) (nn.Dropout).
-// tests/test_lora.py restates the hash in numpy and checks the masks bit-exactly.
+// regenerate the same mask from (seed, token, feature) without storing it. One 32-bit hash per
+// (token, feature pair) gives both features a 16-bit uniform (low half: even feature, high half:
+// odd); an element is kept iff its 16 bits >= thr16 = round(p * 2^16) (p = 0.05 -> 0.0500031);
+// kept values are scaled by 1/(1-p) (nn.Dropout). The per-token part is hashed once per row.
+// (Round 1 hashed every element: ~12 ms of the LoRA step went to it, tools/lora_drop_bench.py.)
+// tests/test_lora.py restates the hash in numpy (oracle lora_keep_mask) and checks the masks
+// bit-exactly.
 DEV uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -37,12 +41,27 @@ DEV uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-DEV uint32_t drop_hash(uint64_t seed, uint32_t token, uint32_t feat) {
-  const uint32_t h = fmix32((uint32_t)seed ^ fmix32(token * 0x9E3779B1u + (uint32_t)(seed >> 32)));
-  return fmix32(h ^ (feat * 0x27D4EB2Fu + 0x165667B1u));
+DEV uint32_t drop_row(uint64_t seed, int64_t token) {
+  return fmix32((uint32_t)seed ^ fmix32((uint32_t)token * 0x9E3779B1u + (uint32_t)(seed >> 32)));
 }
-DEV bool drop_keep(uint64_t seed, uint32_t thr24, int64_t token, int64_t feat) {
-  return (drop_hash(seed, (uint32_t)token, (uint32_t)feat) >> 8) >= thr24;
+DEV uint32_t drop_pair(uint32_t row, int64_t feat) {
+  return fmix32(row ^ ((uint32_t)(feat >> 1) * 0x27D4EB2Fu + 0x165667B1u));
+}
+DEV bool drop_keep(uint64_t seed, uint32_t thr16, int64_t token, int64_t feat) {
+  const uint32_t h = drop_pair(drop_row(seed, token), feat);
+  return ((feat & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr16;
+}
+// kept-element multipliers (scale or 0) of the N consecutive features f0 .. f0+N-1 of one token,
+// f0 and N even: one row hash, N/2 pair hashes
+template <int N>
+DEV void drop_scales(uint64_t seed, uint32_t thr16, float scale, int64_t token, int64_t f0, float (&m)[N]) {
+  const uint32_t row = drop_row(seed, token);
+#pragma unroll
+  for (int j = 0; j < N; j += 2) {
+    const uint32_t h = drop_pair(row, f0 + j);
+    m[j] = (h & 0xFFFFu) >= thr16 ? scale : 0.f;
+    m[j + 1] = (h >> 16) >= thr16 ? scale : 0.f;
+  }
 }
 
 template <typename T> struct Elt;

@@ -116,10 +116,12 @@ DEV void drop_tile(const GemmArgs& p, int64_t idx0, int64_t k0, u16x8 (&r)[4]) {
     int64_t tok, f0;
     if (LAYOUT == 0) { tok = idx0 + (q >> 3); f0 = k0 + (q & 7) * 8; }
     else { tok = k0 + (q >> 4); f0 = idx0 + (q & 15) * 8; }
+    float ms[8];
+    drop_scales<8>(p.drop_seed, p.drop_thr, p.drop_scale, tok, f0, ms);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float v = bf2f(r[i][j]);
-      r[i][j] = drop_keep(p.drop_seed, p.drop_thr, tok, f0 + j) ? f2bf(v * p.drop_scale) : (u16)0;
+      r[i][j] = ms[j] != 0.f ? f2bf(v * ms[j]) : (u16)0;
     }
   }
 }
@@ -206,8 +208,10 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = acc[j] * p.alpha;
   if (p.drop_mode == 3) {
+    float ms[4];
+    drop_scales<4>(p.drop_seed, p.drop_thr, p.drop_scale, m, n, ms);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = drop_keep(p.drop_seed, p.drop_thr, m, n + j) ? v[j] * p.drop_scale : 0.f;
+    for (int j = 0; j < 4; ++j) v[j] = ms[j] != 0.f ? v[j] * ms[j] : 0.f;
   }
   if (p.bias) {
     const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
@@ -272,8 +276,10 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = a[j] * p.alpha;
   if (p.drop_mode == 3) {
+    float ms[8];
+    drop_scales<8>(p.drop_seed, p.drop_thr, p.drop_scale, m, n, ms);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = drop_keep(p.drop_seed, p.drop_thr, m, n + j) ? v[j] * p.drop_scale : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = ms[j] != 0.f ? v[j] * ms[j] : 0.f;
   }
   if (p.bias) {
     const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
@@ -1496,7 +1502,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.addend = (const u16*)d.addend; p.ld_add = d.ld_addend;
   const bool dropping = d.drop_operand != 0 && d.drop_p > 0.f;
   p.drop_mode = dropping ? d.drop_operand : 0;
-  p.drop_thr = (uint32_t)(d.drop_p * 16777216.0f + 0.5f);
+  p.drop_thr = (uint32_t)(d.drop_p * 65536.0f + 0.5f);
   p.drop_scale = dropping ? 1.f / (1.f - d.drop_p) : 1.f;
   p.drop_seed = d.drop_seed;
   p.part = nullptr;

@@ -222,7 +222,7 @@ int cullavo_gemm_f32_impl(const cullavo_gemm_desc& d, hipStream_t s) {
   p.alpha = d.alpha; p.beta = d.beta; p.act = d.act;
   const bool dropping = d.drop_operand != 0 && d.drop_p > 0.f;
   p.drop_mode = dropping ? d.drop_operand : 0;
-  p.drop_thr = (uint32_t)(d.drop_p * 16777216.0f + 0.5f);
+  p.drop_thr = (uint32_t)(d.drop_p * 65536.0f + 0.5f);
   p.drop_scale = dropping ? 1.f / (1.f - d.drop_p) : 1.f;
   p.drop_seed = d.drop_seed;
   if (p.drop_mode == 1) return dispatch_f32<1>(p, d.a_layout, d.b_layout, s);

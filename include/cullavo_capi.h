@@ -73,8 +73,9 @@ int cullavo_gemm(int a_layout, int b_layout, int64_t M, int64_t N, int64_t K,
  *   drop_operand: 0 none; 1 dropout on A (needs a_layout 0, A[m][k] = x[token m][feature k]);
  *           2 on B (needs b_layout 1, B[k][n] = x[token k][feature n]); 3 on the output
  *           (token m, feature n), applied to alpha*A.B^T before bias / beta;
- *   drop_p in [0, 1), drop_seed: element kept iff (hash(seed, token, feature) >> 8) >=
- *           round(drop_p * 2^24), kept values scaled by 1/(1-drop_p) (csrc/common.h drop_hash).
+ *   drop_p in [0, 1), drop_seed: one hash(seed, token, feature / 2) per feature pair; element
+ *           kept iff its 16-bit half (even feature: low, odd: high) >= round(drop_p * 2^16), kept
+ *           values scaled by 1/(1-drop_p) (csrc/common.h drop_row / drop_pair / drop_keep).
  * Operand dropout runs on the register-staged 128x128 kernel. Products whose tile grid cannot
  * fill the GPU but whose K is long (the adapters' r = 64 GEMMs) run split-K when a workspace of
  * cullavo_gemm_workspace(desc) bytes is passed: f32 partials, reduced in a fixed order. */

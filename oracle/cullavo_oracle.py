@@ -296,16 +296,18 @@ def _fmix32(h):
 
 
 def lora_keep_mask(seed: int, rows: int, cols: int, p: float):
-    """numpy restatement of csrc/common.h drop_hash / drop_keep: bool [rows, cols], element
-    (token, feature) kept iff (hash >> 8) >= round(p * 2^24) (float32 arithmetic as in C)."""
+    """numpy restatement of csrc/common.h drop_row / drop_pair / drop_keep: bool [rows, cols];
+    one 32-bit hash per (token, feature pair), element (token, feature) kept iff its 16-bit half
+    (low: even feature, high: odd) >= round(p * 2^16) (float32 arithmetic as in C)."""
     tok = np.arange(rows, dtype=np.uint64)[:, None]
     feat = np.arange(cols, dtype=np.uint64)[None, :]
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     t = _fmix32((tok * np.uint64(0x9E3779B1) + np.uint64(seed >> 32)) & np.uint64(_M32))
-    h = _fmix32(np.uint64(seed & _M32) ^ t)
-    h = _fmix32(h ^ ((feat * np.uint64(0x27D4EB2F) + np.uint64(0x165667B1)) & np.uint64(_M32)))
-    thr = int(np.float32(p) * np.float32(16777216.0) + np.float32(0.5))
-    return (h >> np.uint64(8)) >= np.uint64(thr)
+    row = _fmix32(np.uint64(seed & _M32) ^ t)
+    h = _fmix32(row ^ (((feat >> np.uint64(1)) * np.uint64(0x27D4EB2F) + np.uint64(0x165667B1)) & np.uint64(_M32)))
+    u16 = (h >> (np.uint64(16) * (feat & np.uint64(1)))) & np.uint64(0xFFFF)
+    thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
+    return u16 >= np.uint64(thr)
 
 
 class LoraOracle:
