@@ -52,6 +52,8 @@ struct GemmArgs {
   int sk_dp, sk_units;
   int64_t sk_iters;
   float* sk_ws;       // f32 partials [sk_units][2][512 threads x TMW*TN f32x4], fragment order
+  int group_m;        // 8-wave tile order: > 0 groups of group_m M-tiles sweep N; < 0 groups of
+                      // -group_m N-tiles sweep M
 };
 
 template <typename V>
@@ -671,11 +673,21 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
 // grouped, XCD-friendly tile order: virtual tile index -> (m0, n0)
 template <int BM2, int BN>
 DEV void tile_origin(const GemmArgs& p, int lid, int64_t& m0, int64_t& n0) {
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * p.tiles_n;
+  if (p.group_m < 0) {
+    const int gn = -p.group_m;
+    const int per_group = gn * p.tiles_m;
+    const int group = lid / per_group;
+    const int first_n = group * gn;
+    const int gsize = min(p.tiles_n - first_n, gn);
+    n0 = (int64_t)(first_n + (lid % per_group) % gsize) * BN;
+    m0 = (int64_t)((lid % per_group) / gsize) * BM2;
+    return;
+  }
+  const int gm = p.group_m;
+  const int per_group = gm * p.tiles_n;
   const int group = lid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(p.tiles_m - first_m, GROUP_M);
+  const int first_m = group * gm;
+  const int gsize = min(p.tiles_m - first_m, gm);
   m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
   n0 = (int64_t)((lid % per_group) / gsize) * BN;
 }
@@ -1434,6 +1446,15 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 static int g_force_tile = -1;
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
+// Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
+// step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
+static int g_group_m = -4;
+
+extern "C" int cullavo_gemm_set_group(int group) {
+  const int prev = g_group_m;
+  if (group != 0 && group >= -64 && group <= 64) g_group_m = group;
+  return prev;
+}
 
 extern "C" int cullavo_gemm_set_streamk(int mode) {
   const int prev = g_streamk;
@@ -1511,6 +1532,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.sk_units = 0;
   p.sk_iters = 0;
   p.sk_ws = nullptr;
+  p.group_m = g_group_m;
   {
     auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     p.epi_lds = a16(d.C) && a16(d.bias) && a16(d.preact) && a16(residual) && a16(d.addend) &&

@@ -128,6 +128,10 @@ int cullavo_gemm_set_tile(int mode);
    (2 x 256x256 f32 per CU, allocated at first use); a fix-up kernel adds them in K order.
    Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_streamk(int mode);
+/* Tile order of the 8-wave kernels (tuning/A-B switch): > 0 = groups of that many M-tiles
+   sweep the N-tiles, < 0 = groups of -group N-tiles sweep the M-tiles (default -4); each XCD
+   walks a contiguous run of the order. 0 leaves the setting. Returns the previous setting. */
+int cullavo_gemm_set_group(int group);
 /* Tuning/A-B switch. Bit 0: 1 (default) = the 8-wave kernels stage their epilogue through LDS
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
    Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */

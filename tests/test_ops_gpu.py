@@ -145,6 +145,41 @@ def test_gemm_streamk_tail(M, N, K, al, bl):
     assert torch.equal(outs[2][0], outs[2][1]), "stream-K not reproducible"
 
 
+@pytest.mark.parametrize("M,N,K,al,bl", [(2304, 8192, 1024, 0, 0), (1032, 2056, 4104, 1, 1), (2000, 1544, 520, 0, 1),
+                                          (1000, 4104, 1032, 1, 0)])
+def test_gemm_tile_order_bitwise(M, N, K, al, bl):
+    """The 8-wave kernels' tile order (cullavo_gemm_set_group: groups of M-tiles sweeping N, or of
+    N-tiles sweeping M, ragged last groups included) only moves tiles between CUs: every order
+    gives bitwise the same C. With the stream-K tail the order decides which tiles are split
+    over K (their f32 partials are summed in a different association), so there each order is
+    checked against the product instead."""
+    from cullavo_amd import _lib
+    A = rnd((M, K), 61)
+    B = rnd((N, K), 62)
+    Ad = (A if al == 0 else A.T.contiguous()).to(DEV)
+    Bd = (B if bl == 0 else B.T.contiguous()).to(DEV)
+    L = _lib.lib()
+    prev, prev_sk = L.cullavo_gemm_set_group(-4), L.cullavo_gemm_set_streamk(0)
+    outs = []
+    try:
+        for sk in (0, 2):
+            L.cullavo_gemm_set_streamk(sk)
+            for g in (-4, 4, 1, 3, -1, -3, 8, -64):
+                L.cullavo_gemm_set_group(g)
+                C = torch.full((M, N), float("nan"), dtype=BF, device=DEV)
+                ops().gemm(al, bl, M, N, K, Ad, Ad.stride(0), Bd, Bd.stride(0), C, N)
+                outs.append((sk, g, C))
+    finally:
+        L.cullavo_gemm_set_group(prev)
+        L.cullavo_gemm_set_streamk(prev_sk)
+    close(outs[0][2], A.float() @ B.float().T, 8e-3, f"group -4 {al}{bl} {M}x{N}x{K}")
+    for sk, g, C in outs:
+        if sk == 0:
+            assert torch.equal(C, outs[0][2]), f"tile order {g} changed C"
+        else:
+            close(C, outs[0][2].float(), 8e-3, f"stream-K, tile order {g}")
+
+
 def test_gemm_streamk_epilogues():
     """Stream-K fix-up runs the full epilogue: bias, GELU, residual, preact, bf16 accumulate and
     the f32 beta=1 weight-gradient path, equal to the data-parallel launch within bf16 rounding."""
