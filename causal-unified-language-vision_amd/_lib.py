@@ -85,6 +85,8 @@ def lib():
             L.cullavo_attn_set_bwd_tiles(int(os.environ["CULLAVO_ATTN_BWD_MODE"]))
         if os.environ.get("CULLAVO_GEMM_TILE"):
             L.cullavo_gemm_set_tile(int(os.environ["CULLAVO_GEMM_TILE"]))
+        if os.environ.get("CULLAVO_SPLITK_TARGET"):  # split-K plan A/B (cullavo_gemm_set_splitk_target)
+            L.cullavo_gemm_set_splitk_target(int(os.environ["CULLAVO_SPLITK_TARGET"]))
         if os.environ.get("CULLAVO_GEMM_GROUP"):  # tile-order A/B (cullavo_gemm_set_group)
             L.cullavo_gemm_set_group(int(os.environ["CULLAVO_GEMM_GROUP"]))
     return _lib

@@ -1273,10 +1273,12 @@ int launch8p(GemmArgs p, hipStream_t s) {
 // Split-K plan for the register-staged kernel: products whose 128x128 tile grid cannot fill
 // the 256 CUs but whose K is long (the LoRA adapter GEMMs: N or M = r = 64, K = tokens or
 // features) are cut into K chunks of >= 4 K-tiles, enough of them for ~512 workgroups.
+int g_splitk_blocks = 512;  // target blocks of a split-K launch (cullavo_gemm_set_splitk_target)
+
 int splitk_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
   const int64_t tiles = cdiv(M, BM) * cdiv(N, BN), nk = cdiv(K, BK);
   if (tiles >= 384 || nk < 8) return 1;
-  int64_t s = std::min<int64_t>(std::max<int64_t>(512 / tiles, 2), std::min<int64_t>(nk / 4, 32));
+  int64_t s = std::min<int64_t>(std::max<int64_t>(g_splitk_blocks / tiles, 2), std::min<int64_t>(nk / 4, 32));
   if (s < 2) return 1;
   const int64_t per = cdiv(nk, s);
   s = cdiv(nk, per);
@@ -1449,6 +1451,12 @@ static int g_nt_store = 0;
 // Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
 // step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
 static int g_group_m = -4;
+
+extern "C" int cullavo_gemm_set_splitk_target(int blocks) {
+  const int prev = g_splitk_blocks;
+  if (blocks >= 64 && blocks <= 8192) g_splitk_blocks = blocks;
+  return prev;
+}
 
 extern "C" int cullavo_gemm_set_group(int group) {
   const int prev = g_group_m;

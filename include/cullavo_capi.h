@@ -132,6 +132,10 @@ int cullavo_gemm_set_streamk(int mode);
    sweep the N-tiles, < 0 = groups of -group N-tiles sweep the M-tiles (default -4); each XCD
    walks a contiguous run of the order. 0 leaves the setting. Returns the previous setting. */
 int cullavo_gemm_set_group(int group);
+/* Split-K plan of the small-grid GEMMs (tuning/A-B switch): the number of blocks a split-K
+   launch aims for (default 512 = two 4-wave blocks per CU); out-of-range values leave it.
+   Returns the previous setting. */
+int cullavo_gemm_set_splitk_target(int blocks);
 /* Tuning/A-B switch. Bit 0: 1 (default) = the 8-wave kernels stage their epilogue through LDS
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
    Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */
