@@ -2,7 +2,7 @@
 # Round-2 closing GPU pass on the restored tree: GPU tests, smoke, the bench lines of every
 # BASELINE workload, and a kernel-trace profile of the default bench command.
 set -o pipefail
-OUT=gpurun_out/r02d
+OUT=gpurun_out/${1:-r02d}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -3 $OUT/gpu_tests.log
