@@ -28,6 +28,7 @@ DT_BF16 = 1
 ACT_NONE = 0
 ACT_GELU = 1
 ACT_QUICK_GELU = 2
+ACT_SWIGLU_BWD = 3  # down-proj dX GEMM epilogue writing dgate | dup (CULLAVO_ACT_SWIGLU_BWD)
 
 _lib = None
 _decls: dict[str, tuple[str, list[tuple[str, str]]]] | None = None

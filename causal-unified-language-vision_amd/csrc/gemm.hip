@@ -202,10 +202,42 @@ DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// CULLAVO_ACT_SWIGLU_BWD epilogue for NV consecutive columns: the product is dh = d(silu(g) * u)
+// of the SwiGLU, rounded to bf16 as the unfused path stores it; with g = gu[m][n], u = gu[m][F + n]
+// (gu = p.residual, F = p.N) it writes dg to C[m][n] and du to C[m][F + n], in the arithmetic of
+// swiglu_bwd_k (elementwise.hip) so the fused and unfused paths are bitwise equal.
+DEV float sigmoid_ieee(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int NV>
+DEV void swiglu_bwd_store(const GemmArgs& p, const float* acc, int64_t m, int64_t n) {
+  typedef __attribute__((ext_vector_type(NV))) unsigned short uv_t;
+  const u16* gr = p.residual + m * p.ldr;
+  const uv_t gv = *reinterpret_cast<const uv_t*>(gr + n);
+  const uv_t uv = *reinterpret_cast<const uv_t*>(gr + p.N + n);
+  uv_t oa, ob;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float dv = round_bf(acc[j] * p.alpha);
+    const float g = bf2f(gv[j]), u = bf2f(uv[j]);
+    const float sg = sigmoid_ieee(g);
+    const float silu = g * sg;
+    ob[j] = f2bf(dv * round_bf(silu));
+    oa[j] = f2bf(dv * u * sg * (1.f + g * (1.f - sg)));
+  }
+  u16* cp = (u16*)p.C + m * p.ldc + n;
+  *reinterpret_cast<uv_t*>(cp) = oa;
+  *reinterpret_cast<uv_t*>(cp + p.N) = ob;
+}
+
 // epilogue for one lane's C[m][n .. n+3] (bias -> preact -> act -> residual -> beta -> store)
 template <int CT>
 DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
   if (m >= p.M || n >= p.N) return;
+  if (CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD) {
+    const float a[4] = {acc[0], acc[1], acc[2], acc[3]};
+    swiglu_bwd_store<4>(p, a, m, n);
+    return;
+  }
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = acc[j] * p.alpha;
@@ -274,6 +306,10 @@ DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
 template <int CT>
 DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
   if (m >= p.M || n >= p.N) return;  // N % 8 == 0: the whole group is in range
+  if (CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD) {
+    swiglu_bwd_store<8>(p, a, m, n);
+    return;
+  }
   float v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = a[j] * p.alpha;
@@ -1511,7 +1547,14 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   CV_REQUIRE(lda >= (a_layout == 0 ? K : M) && ldb >= (b_layout == 0 ? K : N) && ldc >= N,
              CULLAVO_EINVAL, "leading dimension too small");
   CV_REQUIRE(c_dtype == CULLAVO_DT_BF16 || c_dtype == CULLAVO_DT_F32, CULLAVO_EUNSUPPORTED, "c_dtype");
-  CV_REQUIRE(act >= CULLAVO_ACT_NONE && act <= CULLAVO_ACT_QUICK_GELU, CULLAVO_EINVAL, "act");
+  CV_REQUIRE(act >= CULLAVO_ACT_NONE && act <= CULLAVO_ACT_SWIGLU_BWD, CULLAVO_EINVAL, "act");
+  if (act == CULLAVO_ACT_SWIGLU_BWD) {
+    CV_REQUIRE(c_dtype == CULLAVO_DT_BF16 && !d.f32_operands, CULLAVO_EUNSUPPORTED, "SwiGLU-backward epilogue is bf16 only");
+    CV_REQUIRE(residual != nullptr && ldr >= 2 * N && ldc >= 2 * N, CULLAVO_EINVAL,
+               "SwiGLU-backward epilogue needs gu (residual) and C of 2N columns");
+    CV_REQUIRE(d.bias == nullptr && d.preact == nullptr && d.addend == nullptr && d.drop_operand == 0 &&
+               d.beta == 0.f, CULLAVO_EINVAL, "SwiGLU-backward epilogue takes no bias/preact/addend/dropout/beta");
+  }
   CV_REQUIRE(d.addend == nullptr || (d.ld_addend % 4 == 0 && d.ld_addend >= N), CULLAVO_EINVAL,
              "ld_addend must be >= N and a multiple of 4");
   CV_REQUIRE(d.drop_operand >= 0 && d.drop_operand <= 3, CULLAVO_EINVAL, "drop_operand");

@@ -21,6 +21,7 @@ import torch
 
 from . import ops
 from .arena import commit, grad_slot, trainable
+from .lora import NO_LORA
 from .ops import ACT_GELU, ACT_QUICK_GELU
 
 
@@ -45,6 +46,9 @@ def _lin_act(x, w, b, act, keep_preact):
 # per CU each) slow each other more than the filled tails gain; with the compute stream at high
 # priority 386.2 vs 388.4 (noise level), so the single stream stays the default.
 DW_STREAM = os.environ.get("CULLAVO_DW_STREAM", "off")
+# SwiGLU backward in the down-projection dX GEMM's epilogue (CULLAVO_FUSED_SWIGLU_BWD=0: the
+# separate swiglu_bwd kernel, for A/B)
+FUSED_SWIGLU_BWD = os.environ.get("CULLAVO_FUSED_SWIGLU_BWD", "1") != "0"
 if DW_STREAM not in ("side", "off"):
     raise ValueError(f"CULLAVO_DW_STREAM={DW_STREAM!r}: expected side | off")
 _DW: dict = {}  # device -> {"stream": side stream, "main": stream to join, "queued": bool}
@@ -183,12 +187,17 @@ class LlamaLayerFn(torch.autograd.Function):
         T, d = h.shape
         H, D = cfg.num_attention_heads, cfg.head_dim
         dh3 = dh3.contiguous()
-        # MLP
-        da = layer.linear_dx(dh3, "down")
-        lg["down"].backward(dh3, a, u_d, da, tr, seed)
+        # MLP. Without a LoRA adapter on down_proj the SwiGLU backward runs in the epilogue of
+        # the down-projection dX GEMM (dh never stored); with one, dh collects the adapter's
+        # share first (bitwise the same arithmetic either way, tests/test_ops_gpu.py).
+        if lg["down"] is NO_LORA and FUSED_SWIGLU_BWD and gu.dtype == torch.bfloat16:
+            dgu = layer.linear_dx(dh3, "down", swiglu_gu=gu)
+        else:
+            da = layer.linear_dx(dh3, "down")
+            lg["down"].backward(dh3, a, u_d, da, tr, seed)
+            dgu = ops.swiglu_bwd(da, gu)
+            del da
         _write_dw(dh3, a, layer.mlp.down_proj.weight)
-        dgu = ops.swiglu_bwd(da, gu)
-        del da
         dx2 = layer.linear_dx(dgu, "gu")
         lg["gu"].backward(dgu, x2, u_gu, dx2, tr, seed)
         if trainable(layer.mlp.gate_proj.weight):

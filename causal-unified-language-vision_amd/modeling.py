@@ -414,12 +414,13 @@ class LlamaDecoderLayer(nn.Module):
         for key, shape in self._kmajor_specs().values():
             self._arena.prefetch_transposed(key, shape, st)
 
-    def linear_dx(self, dy, which: str):
-        """dx = dy @ W for which in qkv | o | gu | down (fused weights), via the K-major copy."""
+    def linear_dx(self, dy, which: str, swiglu_gu=None):
+        """dx = dy @ W for which in qkv | o | gu | down (fused weights), via the K-major copy;
+        swiglu_gu: return swiglu_bwd(dx, gu) from the GEMM epilogue instead (ops.linear_dx)."""
         key, shape = self._kmajor_specs()[which]
         if KMAJOR_MODE == "off":
-            return ops.linear_dx(dy, self._arena.view(key, shape))
-        return ops.linear_dx_t(dy, self._arena.transposed(key, shape))
+            return ops.linear_dx(dy, self._arena.view(key, shape), swiglu_gu=swiglu_gu)
+        return ops.linear_dx_t(dy, self._arena.transposed(key, shape), swiglu_gu=swiglu_gu)
 
     def gu_grad_slot(self):
         g, beta = self._arena.grad_slot(self._lp + "mlp.gate_proj.weight",

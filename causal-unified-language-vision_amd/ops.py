@@ -12,10 +12,10 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, DT_BF16, DT_F32, call, lib
+from ._lib import ACT_GELU, ACT_NONE, ACT_QUICK_GELU, ACT_SWIGLU_BWD, DT_BF16, DT_F32, call, lib
 
 __all__ = [
-    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "gemm", "gemm_ex", "linear", "linear_dx", "linear_dx_t", "transpose2d", "linear_dw",
+    "ACT_NONE", "ACT_GELU", "ACT_QUICK_GELU", "ACT_SWIGLU_BWD", "gemm", "gemm_ex", "linear", "linear_dx", "linear_dx_t", "transpose2d", "linear_dw",
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "swiglu_fwd", "swiglu_bwd",
     "act_bwd", "colsum", "rope", "attn_fwd", "attn_bwd", "embedding_fwd", "embedding_bwd",
     "im2col_patches", "vision_embed_ln", "merge_plan", "row_gather2", "shift_targets", "ce_fwd",
@@ -185,23 +185,38 @@ def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: 
     return (y, pre) if want_preact else y
 
 
-def linear_dx(dy, w, *, residual=None, out=None):
-    """dx = dy @ w (+ residual); dy [M,N], w [N,K] -> [M,K]"""
+def _swiglu_dx(a_layout_b, M, K, N, dy, w, gu):
+    """dgu [M, 2K] = swiglu_bwd(dy @ w, gu) with the SwiGLU backward in the GEMM epilogue."""
+    if gu.shape != (M, 2 * K) or gu.dtype != torch.bfloat16 or dy.dtype != torch.bfloat16:
+        raise ValueError(f"swiglu dx: gu {tuple(gu.shape)} {gu.dtype} vs {(M, 2 * K)} bf16")
+    dgu = torch.empty((M, 2 * K), dtype=dy.dtype, device=dy.device)
+    gemm(0, a_layout_b, M, K, N, dy, _ld(dy), w, _ld(w), dgu, _ld(dgu), act=ACT_SWIGLU_BWD, residual=gu,
+         ldr=_ld(gu))
+    return dgu
+
+
+def linear_dx(dy, w, *, residual=None, out=None, swiglu_gu=None):
+    """dx = dy @ w (+ residual); dy [M,N], w [N,K] -> [M,K]. With swiglu_gu = gu [M, 2K] (the
+    SwiGLU's gate | up) it returns swiglu_bwd(dx, gu) [M, 2K] instead, fused into the GEMM."""
     M, N = dy.shape
     K = w.shape[1]
+    if swiglu_gu is not None:
+        return _swiglu_dx(1, M, K, N, dy, w, swiglu_gu)
     dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
     gemm(0, 1, M, K, N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), residual=residual,
          ldr=_ld(residual) if residual is not None else 0)
     return dx
 
 
-def linear_dx_t(dy, wt, *, residual=None, out=None):
+def linear_dx_t(dy, wt, *, residual=None, out=None, swiglu_gu=None):
     """dx = dy @ wt.T (+ residual); dy [M,N], wt [K,N] (the K-major copy of w [N,K], ParamArena
     .transposed): both operands reduction-contiguous, bitwise equal to linear_dx(dy, w)."""
     M, N = dy.shape
     K = wt.shape[0]
     if wt.shape[1] != N:
         raise ValueError(f"linear_dx_t: dy {tuple(dy.shape)} vs wt {tuple(wt.shape)}")
+    if swiglu_gu is not None:
+        return _swiglu_dx(0, M, K, N, dy, wt, swiglu_gu)
     dx = out if out is not None else torch.empty((M, K), dtype=dy.dtype, device=dy.device)
     gemm(0, 0, M, K, N, dy, _ld(dy), wt, _ld(wt), dx, _ld(dx), residual=residual,
          ldr=_ld(residual) if residual is not None else 0)

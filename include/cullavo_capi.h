@@ -41,6 +41,12 @@ extern "C" {
 #define CULLAVO_ACT_NONE 0
 #define CULLAVO_ACT_GELU 1       /* erf GELU: LlavaMultiModalProjector act (tf:llava/modeling_llava.py:99) */
 #define CULLAVO_ACT_QUICK_GELU 2 /* x*sigmoid(1.702x): CLIPMLP act (tf:activations.py:117-123) */
+/* SwiGLU backward fused into the epilogue of the down-projection dX GEMM (LlamaMLP.down_proj
+   input gradient, tf:llama/modeling_llama.py:MLP): the product dh [M][N] (rounded to bf16) is not
+   stored; with gu = residual [M][2N] (gate | up, ldr >= 2N) C [M][2N] (ldc >= 2N) receives
+   dgate | dup exactly as cullavo_swiglu_bwd(dh, gu) writes them. bf16 only, no bias / preact /
+   addend / dropout / beta. */
+#define CULLAVO_ACT_SWIGLU_BWD 3
 
 int cullavo_abi_version(void);
 const char* cullavo_last_error(void);

@@ -160,6 +160,27 @@ def test_kmajor_weight_copies_bitwise_and_refreshed(monkeypatch):
             assert torch.equal(a, b), f"mode {mode} step {s}"
 
 
+def test_fused_swiglu_bwd_bitwise(monkeypatch):
+    """The decoder layers' SwiGLU backward fused into the down-projection dX GEMM epilogue
+    (functions.FUSED_SWIGLU_BWD, the default) gives gradients bitwise equal to the separate
+    swiglu_bwd kernel (full fine-tune; with a LoRA adapter on down_proj the unfused path runs)."""
+    import cullavo_amd.functions as FN
+    ids, mask, pix, labels = inputs()
+    for trainable in ("full",):
+        grads = {}
+        for fused in (True, False):
+            monkeypatch.setattr(FN, "FUSED_SWIGLU_BWD", fused)
+            m = build(trainable=trainable)
+            out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
+            out.loss.backward()
+            torch.cuda.synchronize()
+            grads[fused] = {k: a.grad_flat.clone() for k, a in m.arenas.items()
+                            if getattr(a, "grad_flat", None) is not None}
+        assert grads[True].keys() == grads[False].keys()
+        for k in grads[True]:
+            assert torch.equal(grads[True][k], grads[False][k]), f"{trainable} arena {k}"
+
+
 def test_dw_side_stream_bitwise(monkeypatch):
     """Weight-gradient GEMMs on the side stream (functions.DW_STREAM "side") give gradients and
     AdamW updates bitwise equal to the single-stream path, read on the compute stream right

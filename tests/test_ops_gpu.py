@@ -347,6 +347,30 @@ def test_swiglu():
     close(dgu[:, Fd:], u.grad, 1e-2, "dup")
 
 
+@pytest.mark.parametrize("M,Fd,d,tile", [(8704, 11008, 4096, -1), (1000, 1376, 520, -1), (520, 688, 264, 0),
+                                         (1000, 1376, 520, 2), (1000, 1376, 520, 3), (40, 688, 4104, -1)])
+def test_swiglu_bwd_fused_in_dx_gemm(M, Fd, d, tile):
+    """The down-projection dX GEMM with the SwiGLU backward in its epilogue (ACT_SWIGLU_BWD) is
+    bitwise equal to dh = dy @ W_down then swiglu_bwd(dh, gu): the 7B shape, ragged tiles, the
+    4-wave / 256x256 / 192x256 kernels (tile modes 0 / 2 / 3), the split-K small-M launch, and
+    both weight layouts (W and its K-major copy)."""
+    from cullavo_amd import _lib
+    dy = rnd((M, d), 71).to(DEV)
+    w = rnd((d, Fd), 72, 0.05).to(DEV)          # down_proj.weight [d, F]
+    gu = rnd((M, 2 * Fd), 73, 2.0).to(DEV)
+    prev = _lib.lib().cullavo_gemm_set_tile(tile)
+    try:
+        ref = ops().swiglu_bwd(ops().linear_dx(dy, w), gu)
+        fused = ops().linear_dx(dy, w, swiglu_gu=gu)
+        fused_t = ops().linear_dx_t(dy, w.t().contiguous(), swiglu_gu=gu)
+    finally:
+        _lib.lib().cullavo_gemm_set_tile(prev)
+    assert torch.equal(fused, ref)
+    assert torch.equal(fused_t, ref)
+    with pytest.raises(Exception):
+        ops().linear_dx(dy, w, swiglu_gu=gu[:, :Fd])
+
+
 @pytest.mark.parametrize("act", [1, 2])
 def test_act_bwd(act):
     x = rnd((33, 256), 50, 2.0)
