@@ -66,6 +66,11 @@ def declarations():
     return _decls
 
 
+def abi_version(path: str = HEADER) -> int:
+    """CULLAVO_ABI_VERSION of the header the binding is generated from."""
+    return int(re.search(r"#define CULLAVO_ABI_VERSION (\d+)", open(path).read()).group(1))
+
+
 def lib():
     """Load and bind the HIP library (raises if it is absent: there is no CPU fallback)."""
     global _lib
@@ -76,6 +81,10 @@ def lib():
                 "(python -c 'import __graft_entry__ as g; g.build()')"
             )
         L = ctypes.CDLL(LIB_PATH)
+        L.cullavo_abi_version.restype = ctypes.c_int
+        if L.cullavo_abi_version() != abi_version():
+            raise RuntimeError(f"{LIB_PATH} was built for ABI {L.cullavo_abi_version()} but "
+                               f"{HEADER} declares ABI {abi_version()}: rebuild the library")
         for name, (ret, params) in declarations().items():
             fn = getattr(L, name)
             fn.argtypes = [_argtype(t) for t, _ in params]

@@ -15,5 +15,5 @@ int cullavo_check_launch(const char* what) {
   return CULLAVO_OK;
 }
 
-extern "C" int cullavo_abi_version(void) { return 1; }
+extern "C" int cullavo_abi_version(void) { return CULLAVO_ABI_VERSION; }
 extern "C" const char* cullavo_last_error(void) { return g_last_error.c_str(); }

@@ -20,7 +20,13 @@ per step by the fused backward Functions, so a bucket is just a slice of that bu
    stream also waits for that stream before each bucket;
  * finish() zero-commits what the backward did not write (arena.finalize_grads), launches
    the remaining buckets and makes the compute stream wait for the comm stream, so the
-   optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics.
+   optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics;
+ * which keys the optimizer skips is agreed across ranks: a per-key "written on this rank"
+   mask is MAX-reduced over a host (gloo) group, so a key no rank wrote (e.g. the projector
+   when no rank's batch holds an image) stays skipped exactly as on one GPU (DDP leaves such a
+   gradient None and torch AdamW skips it); a key written by any rank gets the averaged
+   gradient and a step. The mask is host-side control flow, so the exchange never waits on
+   the GPU.
 The same asynchronous code runs on every backend: RCCL reduces with ReduceOp.AVG; gloo (the
 CPU tests) sums and the 1/N scale is applied in finish() after the waits.
 """
@@ -63,6 +69,16 @@ class GradReducer:
         dev = arenas[0].flat.device if arenas else torch.device("cpu")
         self.stream = torch.cuda.Stream(device=dev) if (use_side_stream and dev.type == "cuda") else None
         self.enabled = self.world > 1 if enabled is None else (bool(enabled) and dist.is_initialized())
+        # host group for the written-key mask: the process group itself when it is gloo, else a
+        # gloo group over the same ranks (created collectively here, as every rank builds its
+        # reducer at the same point of init)
+        self._host_group = None
+        if dist.is_initialized():
+            if backend == "gloo":
+                self._host_group = group
+            else:
+                ranks = dist.get_process_group_ranks(group) if group is not None else None
+                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
         self.reset()
 
     def _add_bucket(self, ai, ar, keys):
@@ -121,6 +137,18 @@ class GradReducer:
         op = dist.ReduceOp.AVG if self.avg_supported else dist.ReduceOp.SUM
         return dist.all_reduce(view, op=op, group=self.group, async_op=True)
 
+    def _agree_skipped(self):
+        """ar.skipped := the keys no rank wrote this cycle (MAX of the per-rank written masks)."""
+        keys = [(ar, k) for ar in self.arenas for k in ar.offsets]
+        written = torch.tensor([0 if k in ar.skipped else 1 for ar, k in keys], dtype=torch.uint8)
+        if self._host_group is not None or dist.is_initialized():
+            dist.all_reduce(written, op=dist.ReduceOp.MAX, group=self._host_group)
+        for ar in self.arenas:
+            ar.skipped = set()
+        for (ar, k), w in zip(keys, written.tolist()):
+            if not w:
+                ar.skipped.add(k)
+
     def finish(self):
         """Zero-commit unwritten gradients, issue every bucket not yet reduced (in order) and
         make the current stream wait for all of them (sum backends: scale by 1/N after)."""
@@ -128,9 +156,7 @@ class GradReducer:
             return
         for ar in self.arenas:
             ar.finalize_grads()  # commits the keys it zeroes -> hooks issue their buckets
-            # after the exchange every rank holds a defined (averaged) gradient for every key,
-            # as under DDP: nothing is skipped by the optimizer in DP mode
-            ar.skipped = set()
+        self._agree_skipped()
         for b in self.buckets:
             b["pending"].clear()
         self._issue_ready()

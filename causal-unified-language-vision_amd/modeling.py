@@ -284,7 +284,14 @@ class CLIPVisionTransformer(nn.Module):
                                         cfg.layer_norm_eps)
         self.kpad = int(math.ceil(cfg.num_channels * cfg.patch_size ** 2 / 64) * 64)
         self._arena = arena
+        self._prefix = prefix
         self._wpad = None  # (arena state it was packed from, [d, kpad] patch weight)
+
+    def _wait(self, *parts):
+        """pending optimizer updates (FusedAdamW overlap) of these parameter groups: a trainable
+        tower's embeddings / pre- / post-layernorm are read here, not in a layer's run()"""
+        for part in parts:
+            self._arena.wait_update(*self._arena.span(self._prefix + part))
 
     def packed_patch_weight(self):
         """Conv2d weight [d, C, p, p] as a K-padded GEMM operand [d, kpad], packed once and
@@ -305,6 +312,7 @@ class CLIPVisionTransformer(nn.Module):
                              f"match model ({cfg.image_size}*{cfg.image_size}).")
         if pixel_values.dtype not in (torch.float32, torch.bfloat16):
             pixel_values = pixel_values.float()
+        self._wait("embeddings.", "pre_layrnorm.")
         patches = ops.im2col_patches(pixel_values, cfg.patch_size, self.kpad, dtype=self._arena.dtype)
         x = ops.linear(patches, self.packed_patch_weight())
         T = cfg.num_patches + 1
@@ -326,6 +334,7 @@ class CLIPVisionTransformer(nn.Module):
             h = layer.run(h, B, T)
             hs.append(h.view(B, T, -1))
         last = hs[-1]
+        self._wait("post_layernorm.")
         pooled = self.post_layernorm(last[:, 0, :])
         return CLIPVisionOutput(last, pooled, tuple(hs) if output_hidden_states else None)
 

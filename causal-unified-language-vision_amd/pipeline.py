@@ -201,7 +201,10 @@ class CuLLaVOPipeline:
             loss_info = {k: v.detach().item() for k, v in loss.items()}
         else:
             loss_info = {k: v.detach() for k, v in loss.items()}
-        sample_size_info = {"num_samples": int(batch["input_ids"].shape[0])}
+        # raw record lists (the reference's collate=list batches, CuLLaVOPipeline.py:85 len(batch))
+        # or pre-tokenised tensor dicts
+        n = len(batch) if isinstance(batch, (list, tuple)) else int(batch["input_ids"].shape[0])
+        sample_size_info = {"num_samples": n}
         total = sum(loss.values())
         if total.requires_grad:
             trainer.backward_loss(total)

@@ -344,6 +344,12 @@ def step2_preprocess(model, batched_inputs, processor, device, *, dice=None, gen
             boxes, classes, flag = box_and_class_parser(text)
             if flag:
                 continue  # the reference drops the record (:372-373)
+            if len(classes) > len(COLOR_LIST):
+                # the reference draws box_tensor[:len(color_list)] with labels=class_list at full
+                # length: detectron2's overlay_instances asserts len(labels) == num_instances
+                # (utils/visualizer.py:673) and the bare except emits the record without boxes
+                new.append(base)
+                continue
             new.append(dict(base, boxes=boxes.cpu().tolist(), classes=classes))
         except Exception:  # the reference's bare except (:387-388)
             new.append(base)

@@ -48,6 +48,11 @@ extern "C" {
    addend / dropout / beta. */
 #define CULLAVO_ACT_SWIGLU_BWD 3
 
+/* ABI version: bumped whenever an exported signature changes (2: cullavo_im2col_patches gained
+   out_dtype, cullavo_vision_embed_ln dtype, cullavo_gemm_desc f32_operands). A consumer built
+   against this header checks cullavo_abi_version() == CULLAVO_ABI_VERSION at load. */
+#define CULLAVO_ABI_VERSION 2
+
 int cullavo_abi_version(void);
 const char* cullavo_last_error(void);
 

@@ -160,6 +160,87 @@ def test_grad_reducer_ragged_ranks_gloo_world2():
     assert out[0][3] == out[1][3] == []  # DP: every key steps on the averaged gradient
 
 
+def _world_worker(rank, world, port, q):
+    """N ranks, each writing its gradients in its own (seeded) order. 'proj.w' is written only by
+    even ranks (odd ranks: a batch with no image), 'unused.w' by no rank, and 'layers.1.w' only by
+    the last rank (a ragged batch that alone reaches a parameter)."""
+    import sys
+    sys.path.insert(0, REPO)
+    try:
+        _init(rank, world, port)
+        from cullavo_amd.arena import ParamArena
+        from cullavo_amd.dist import GradReducer
+        from cullavo_amd.optim import FusedAdamW
+        specs = [(f"layers.{i}.w", (16, 8)) for i in range(6)] + [("proj.w", (8, 8)), ("unused.w", (4, 8))]
+        ar = ParamArena("layers", specs, device="cpu", dtype=torch.float32, trainable=True)
+        red = GradReducer([ar], bucket_bytes=2 * 16 * 8 * 4)
+        issued = []
+        orig = red._launch
+
+        def spy(bi):
+            issued.append(bi)
+            orig(bi)
+        red._launch = spy
+        keys = [f"layers.{i}.w" for i in range(6) if i != 1]
+        if rank % 2 == 0:
+            keys.append("proj.w")
+        if rank == world - 1:
+            keys.append("layers.1.w")
+        g = torch.Generator().manual_seed(1000 + rank)
+        order = [keys[i] for i in torch.randperm(len(keys), generator=g).tolist()]
+        vals = {}
+        for key in order:
+            slot, _ = ar.grad_slot(key)
+            vals[key] = torch.randn(slot.shape, generator=g)
+            slot.copy_(vals[key])
+            ar.commit([key])
+        red.finish()
+        res = {k: ar.params[k].grad.clone().numpy() for k in ar.offsets}
+        steps = {k: 0 for k in ar.offsets}
+        runs = FusedAdamW._runs(ar, steps)  # the element ranges the optimizer would update
+        q.put((rank, res, {k: v.numpy() for k, v in vals.items()}, issued, sorted(ar.skipped), runs))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None, None, None))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_grad_reducer_worlds_ragged_and_unused(world):
+    """DP protocol at the world sizes the scaling run uses: every rank issues the same bucket
+    sequence in the fixed global order whatever order its backward wrote in; the result is the
+    mean over ranks with zeros from ranks that did not reach a parameter; a parameter that no
+    rank wrote stays skipped on every rank (no AdamW step, like torch AdamW on a None grad under
+    DDP), while one written by a single rank is stepped everywhere."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_world_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        rank, res, vals, issued, skipped, runs = q.get(timeout=240)
+        assert vals is not None, res
+        out[rank] = (res, vals, issued, skipped, runs)
+    for p in ps:
+        p.join(timeout=60)
+    for k in out[0][0]:
+        tot = sum(out[r][1].get(k, np.zeros_like(out[0][0][k])) for r in range(world))
+        for r in range(world):
+            np.testing.assert_allclose(out[r][0][k], tot / world, rtol=1e-5, atol=1e-6)
+    nb = len(out[0][2])
+    assert nb >= 3
+    for r in range(world):
+        assert out[r][2] == list(range(nb)), (r, out[r][2])
+        assert out[r][3] == ["unused.w"], (r, out[r][3])
+        assert out[r][4] == out[0][4]
+    # the optimizer's ranges stop before 'unused.w' (the last key) and cover everything else
+    lo, hi = out[0][4][0][0], out[0][4][-1][1]
+    assert lo == 0 and hi == 6 * 16 * 8 + 8 * 8
+
+
 def _dp_worker(rank, world, port, q, text_only_rank=-1):
     import sys
     sys.path.insert(0, REPO)

@@ -67,6 +67,26 @@ def test_step2_preprocess_passthrough_records():
                    {"id": "q1", "image": "a.jpg", "conversations": recs[1]["question"]}]
 
 
+@pytest.mark.parametrize("n_boxes", [20, 21])
+def test_step2_preprocess_more_boxes_than_colors(monkeypatch, n_boxes):
+    """More parsed boxes than the reference's 20 colours: its overlay_instances call trips the
+    labels-length assert and the bare except emits the record without boxes/classes
+    (reference cullavo/arch_cullavo.py:376-389); 20 boxes still produce a box entry."""
+    from cullavo_amd import prompting as P
+    text = "Sure. " + ", ".join(f"obj{i} (#{i}) [0.{i:02d}0, 0.100, 0.500, 0.900]" for i in range(n_boxes))
+    monkeypatch.setattr(P, "eval_process", lambda **kw: {})
+    model = SimpleNamespace(config=SimpleNamespace(ignore_index=-100), generate=lambda **kw: torch.zeros(1, 3))
+    proc = SimpleNamespace(batch_decode=lambda ids, skip_special_tokens=True: [text])
+    rec = {"question_id": "q", "image_id": "a.jpg", "image": torch.zeros(3, 8, 8, dtype=torch.uint8),
+           "question": [{"from": "human", "value": "<image>"}]}
+    out = P.step2_preprocess(model, [rec], proc, "cpu", dice=lambda r: 0)
+    base = {"id": "q", "image": "a.jpg", "conversations": rec["question"]}
+    if n_boxes > len(P.COLOR_LIST):
+        assert out == [base]
+    else:
+        assert out[0]["classes"] == [f"#{i}" for i in range(n_boxes)] and len(out[0]["boxes"]) == n_boxes
+
+
 def _processor(size):
     from cullavo_amd.prompting import ClipImageProcessorHIP, CuLLaVOProcessor
     return CuLLaVOProcessor(TinyVocabTokenizer(), ClipImageProcessorHIP(shortest_edge=size, crop_size=size))

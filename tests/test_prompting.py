@@ -121,3 +121,48 @@ def test_step2_process_on_gpu_with_hip_image_processor():
     assert out["input_ids"].tolist() == g["input_ids"] and out["labels"].tolist() == g["labels"]
     for pv in out["pixel_values"]:
         assert hashlib.sha256(pv.cpu().numpy().astype(np.float32).tobytes()).hexdigest() == c["sha256"]
+
+
+def test_pipeline_forward_step_on_raw_step2_records():
+    """CuLLaVOPipeline.forward_step on the reference's collate=list batches (raw lbk records):
+    the records go through step2_process, the loss is backpropagated and num_samples is
+    len(batch) (reference pipeline/CuLLaVOPipeline.py:76-93, :85). The model is a host stub
+    (the GPU model has its own tests); this pins the pipeline plumbing."""
+    import types
+    from torch import nn
+    from cullavo_amd import prompting as P
+    from cullavo_amd.pipeline import CuLLaVO, CuLLaVOPipeline
+
+    class _StubModel(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = nn.Parameter(torch.ones(()))
+            self.arenas = {}
+            self.seen = None
+
+        def step2_process(self, batch, processor, device):
+            return P.step2_process(batch, processor, device)
+
+        def forward(self, input_ids=None, labels=None, **kw):
+            self.seen = input_ids
+            return types.SimpleNamespace(loss=self.w * (labels != -100).sum().float())
+
+    stub = _StubModel()
+    model = CuLLaVO({"NAME": "cullavo_step2.yaml"}, stub, cullavo_processor=_processor())
+    model.train()
+    calls = []
+    accel = types.SimpleNamespace(device=torch.device("cpu"), sync_gradients=True,
+                                  clip_grad_norm_=lambda p, m: calls.append(("clip", m)))
+    trainer = types.SimpleNamespace(model=types.SimpleNamespace(cullavo_model=stub), accel=accel)
+    trainer.compute_loss = lambda f, b: f(trainer, b)
+    trainer.backward_loss = lambda loss: (loss.backward(), calls.append("backward"))
+    trainer.update_model = lambda: calls.append("update")
+    pipe = CuLLaVOPipeline({"OPTIMIZER": {"GRAD_MAX": 10.0}})
+    pipe.forward_func = lambda tr, b: model(b, tr.accel)  # instance attribute: not bound
+    batch = [dict(r, image=torch.zeros(3, 8, 8, dtype=torch.uint8)) for r in GOLD["records"]]
+    loss_info, size_info, _ = pipe.forward_step(trainer, batch)
+    assert size_info == {"num_samples": len(batch)}
+    assert stub.seen.tolist() == GOLD["prompts"]["right"]["input_ids"]
+    n_sup = sum(x != -100 for row in GOLD["prompts"]["right"]["labels"] for x in row)
+    assert float(loss_info["loss_llm"]) == n_sup and float(stub.w.grad) == n_sup
+    assert calls == ["backward", ("clip", 10.0), "update"]
