@@ -10,7 +10,11 @@ output, residual add and norm output rounds to bf16 where the reference's bf16-c
 under bf16 autocast rounds (reference cullavo/load_cullavo.py:123-126,
 configs/accel/ddp_accel.yaml:8), RMSNorm keeps f32 statistics and casts before the weight
 (tf:llama :63-67), RoPE casts its f32 cos/sin to bf16 (:121-125), attention keeps FA2's f32
-scores/softmax with bf16 P, and the loss upcasts the bf16 logits to f32 (4.37):
+scores/softmax with bf16 P, and the loss upcasts the bf16 logits to f32 (4.37). Every bf16
+product (Linear, patch conv, attention PV) accumulates in f32 and rounds its output once, the
+arithmetic of the reference's bf16 GEMMs on a GPU (hipBLASLt/cuBLAS bf16 with f32 accumulate and
+the bias in the epilogue); torch's CPU bf16 matmul blocks the reduction differently, which alone
+moves the small_gpu logits by rel-L2 8.3e-3 (tools/bf16_noise_floor.py):
 
 * ``forward``          — reference cullavo/arch_cullavo.py:546-677 (CuLLaVOModel.forward):
                           embed :582, vision tower :586, feature select :588-597,
@@ -226,6 +230,13 @@ def make_inputs(cfg: CuLLaVOCfg, batch: int, text_len: int, image_col: int, seed
 # ---------------------------------------------------------------------------------------------
 # ops
 # ---------------------------------------------------------------------------------------------
+def linear(x, w, b=None):
+    """F.linear; bf16 operands accumulate in f32 and round once (a GPU bf16 GEMM + bias epilogue)"""
+    if x.dtype == torch.bfloat16:
+        return F.linear(x.float(), w.float(), None if b is None else b.float()).to(torch.bfloat16)
+    return F.linear(x, w, b)
+
+
 def rmsnorm(x, w, eps):
     """tf:models/llama/modeling_llama.py:53-70: f32 statistics, then weight * x.to(input dtype)
     (a no-op cast in f32; the bf16 rounding point in the bf16-faithful mode)"""
@@ -272,6 +283,8 @@ def attention(q, k, v, scale, allowed=None):
         p = torch.nan_to_num(p, nan=0.0)
     else:
         p = torch.softmax(s.float(), dim=-1)
+    if v.dtype == torch.bfloat16:  # bf16 P, f32 accumulation (FA2 / the flash kernels)
+        return torch.matmul(p.to(v.dtype).float(), v.float()).to(v.dtype)
     return torch.matmul(p.to(v.dtype), v)
 
 
@@ -320,7 +333,7 @@ class LoraOracle:
 
 def lora_linear(x, W, path: str, lora: LoraOracle | None, bias: bool = False):
     """peft LoraLayer.forward around F.linear (bias='none': the adapters carry no bias)."""
-    y = F.linear(x, W[path + ".weight"], W[path + ".bias"] if bias else None)
+    y = linear(x, W[path + ".weight"], W[path + ".bias"] if bias else None)
     if lora is None or f"{path}.lora_A.{lora.adapter}.weight" not in W:
         return y
     A, B = W[f"{path}.lora_A.{lora.adapter}.weight"], W[f"{path}.lora_B.{lora.adapter}.weight"]
@@ -329,7 +342,7 @@ def lora_linear(x, W, path: str, lora: LoraOracle | None, bias: bool = False):
     if mask is not None:
         m = torch.as_tensor(mask, dtype=x.dtype).reshape(*x.shape[:-1], x.shape[-1])
         xd = x * m / (1.0 - lora.p)
-    return y + F.linear(F.linear(xd, A), B) * lora.scaling
+    return y + linear(linear(xd, A), B) * lora.scaling
 
 
 def clip_layer(h, W, prefix, cfg: VisionCfg, lora: LoraOracle | None = None):
@@ -358,7 +371,11 @@ def vision_hidden_states(pixel_values, W, cfg: VisionCfg, n_layers: int | None =
     (pre_layrnorm output, layer 1 output, ..., layer n output)."""
     vp = "vision_tower.vision_model."
     B = pixel_values.shape[0]
-    pe = F.conv2d(pixel_values, W[vp + "embeddings.patch_embedding.weight"], stride=cfg.patch_size)
+    wpe = W[vp + "embeddings.patch_embedding.weight"]
+    if wpe.dtype == torch.bfloat16:  # the conv as a GEMM: f32 accumulation, one rounding
+        pe = F.conv2d(pixel_values.float(), wpe.float(), stride=cfg.patch_size).to(torch.bfloat16)
+    else:
+        pe = F.conv2d(pixel_values, wpe, stride=cfg.patch_size)
     pe = pe.flatten(2).transpose(1, 2)
     cls = W[vp + "embeddings.class_embedding"].expand(B, 1, -1)
     emb = torch.cat([cls, pe], dim=1) + W[vp + "embeddings.position_embedding.weight"][None]
@@ -373,9 +390,9 @@ def vision_hidden_states(pixel_values, W, cfg: VisionCfg, n_layers: int | None =
 
 def projector(x, W):
     """LlavaMultiModalProjector: linear_1 -> GELU(erf) -> linear_2"""
-    x = F.linear(x, W["multi_modal_projector.linear_1.weight"], W["multi_modal_projector.linear_1.bias"])
+    x = linear(x, W["multi_modal_projector.linear_1.weight"], W["multi_modal_projector.linear_1.bias"])
     x = F.gelu(x)
-    return F.linear(x, W["multi_modal_projector.linear_2.weight"], W["multi_modal_projector.linear_2.bias"])
+    return linear(x, W["multi_modal_projector.linear_2.weight"], W["multi_modal_projector.linear_2.bias"])
 
 
 def merge(image_features, inputs_embeds, input_ids, attention_mask, cfg: CuLLaVOCfg, labels=None):
@@ -502,7 +519,7 @@ def forward(W, cfg: CuLLaVOCfg, input_ids, pixel_values, attention_mask=None, la
     if labels is None:
         labels = torch.full_like(mask, cfg.ignore_index).to(torch.long)
     hidden, lm_hs = llama_hidden(embeds, mask, pos, W, cfg.text, lora)
-    logits = F.linear(hidden, W["language_model.lm_head.weight"]).float()
+    logits = linear(hidden, W["language_model.lm_head.weight"]).float()
     loss = shifted_ce(logits, labels, mask)
     return loss, logits, {"attention_mask": mask, "position_ids": pos, "image_features": image_features,
                           "inputs_embeds": embeds, "hidden": hidden}

@@ -225,25 +225,32 @@ def _lora_oracle_masks(model, sctx_seed, n_tokens):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dropout", [0.0, 0.05])
-def test_model_lora_step_matches_oracle(dropout):
+@pytest.mark.parametrize("dtype,dropout", [("bf16", 0.0), ("bf16", 0.05), ("f32", 0.0), ("f32", 0.05)])
+def test_model_lora_step_matches_oracle(dtype, dropout):
+    """The reference's recipe (LoRA r=64 / alpha 16 on the LM and ViT layers, trainable projector,
+    lm_head) through the whole model vs the peft restatement: bf16 production mode against the
+    bf16-faithful oracle (logits / loss <= 1e-2, gradients <= 2e-2), f32 parity mode against the
+    fp32 oracle at the north star's 1e-3 (loss 1e-4)."""
     from cullavo_amd.arch_cullavo import CuLLaVOModel
     from cullavo_amd.config import tiny_gpu
     from cullavo_amd.lora import LoraSettings
+    f32 = dtype == "f32"
+    tol_out, tol_loss, tol_grad = (1e-3, 1e-4, 1e-3) if f32 else (1e-2, 1e-2, 2e-2)
     cfg = O.config_small_gpu()
     W = O.make_weights(cfg, 4)
     s = LoraSettings(r=64, lora_alpha=16.0, lora_dropout=dropout, vision_layers=(1, 2))
-    m = CuLLaVOModel(tiny_gpu(), device="cuda", trainable="lora", init="random", lora=s, seed=9)
+    m = CuLLaVOModel(tiny_gpu(), device="cuda", trainable="lora", init="random", lora=s, seed=9,
+                     dtype=torch.float32 if f32 else torch.bfloat16)
     m.load_state_dict(W, strict=False)
     # non-zero lora_B so every adapter term and gradient is exercised
     with torch.no_grad():
         g = torch.Generator(device="cuda").manual_seed(3)
         for k, p in m.arenas["lora"].params.items():
             if ".lora_B." in k:
-                p.normal_(0.0, 0.05, generator=g)
-    Wl = dict(W)
+                p.copy_(torch.randn(p.shape, device="cuda", generator=g) * 0.05)
+    Wl = dict(W) if f32 else O.to_bf16(W)
     for k, p in m.arenas["lora"].params.items():
-        Wl[k] = p.detach().float().cpu().clone().requires_grad_(True)
+        Wl[k] = p.detach().cpu().clone().requires_grad_(True)
     for k in ("multi_modal_projector.linear_1.weight", "language_model.lm_head.weight"):
         Wl[k] = Wl[k].clone().requires_grad_(True)
     ids, mask, pix, labels = O.make_inputs(cfg, 2, 40, 4, 7)
@@ -259,10 +266,10 @@ def test_model_lora_step_matches_oracle(dropout):
     lv = O.LoraOracle("step1", s.scaling, 0.0, {})  # vision tower in eval(): no dropout
     loss_ref, logits_ref, aux = O.forward(Wl, cfg, ids, pix, mask, labels, lora=lo, vision_lora=lv)
     loss_ref.backward()
-    assert abs(out.loss.item() - loss_ref.item()) <= 3e-2, (out.loss.item(), loss_ref.item())
+    assert abs(out.loss.item() - loss_ref.item()) <= tol_loss, (out.loss.item(), loss_ref.item())
     valid = aux["attention_mask"].bool()
-    a, b = out.logits.detach().float().cpu()[valid], logits_ref.detach()[valid]
-    assert ((a - b).norm() / b.norm()).item() <= 3e-2
+    a, b = out.logits.detach().double().cpu()[valid], logits_ref.detach().double()[valid]
+    assert ((a - b).norm() / b.norm()).item() <= tol_out
     checked = 0
     for k, p in m.arenas["lora"].params.items():
         ref = Wl[k].grad
@@ -270,13 +277,13 @@ def test_model_lora_step_matches_oracle(dropout):
             assert float(p.grad.float().abs().max()) == 0.0, k
             checked += 1
             continue
-        err = ((p.grad.float().cpu() - ref).norm() / (ref.norm() + 1e-12)).item()
-        assert err <= 6e-2, (k, err)
+        err = ((p.grad.double().cpu() - ref.double()).norm() / (ref.double().norm() + 1e-12)).item()
+        assert err <= tol_grad, (k, err)
         checked += 1
     assert checked == len(m.arenas["lora"].params)
     for k in ("multi_modal_projector.linear_1.weight", "language_model.lm_head.weight"):
         p = m.arenas["projector" if k.startswith("multi") else "head"].params[k]
-        err = ((p.grad.float().cpu() - Wl[k].grad).norm() / Wl[k].grad.norm()).item()
-        assert err <= 6e-2, (k, err)
+        err = ((p.grad.double().cpu() - Wl[k].grad.double()).norm() / Wl[k].grad.double().norm()).item()
+        assert err <= tol_grad, (k, err)
     # base weights stay frozen
     assert not m.arenas["layers"].trainable and not m.arenas["vision"].trainable

@@ -1,10 +1,15 @@
-"""End-to-end parity of CuLLaVOModel (bf16 on the gfx950 kernels) against the reference's own
-forward/backward (golden fixtures from tests/golden/make_golden.py) and the CPU oracle.
+"""End-to-end parity of CuLLaVOModel (bf16 on the gfx950 kernels) against the bf16-faithful
+oracle (oracle/cullavo_oracle.py on the reference's bf16 rounding points, autograd for the
+gradients) and the reference's own fp32 forward/backward (golden fixtures from
+tests/golden/make_golden.py).
 
-Gate (bf16 production mode, SURVEY.md §7 "Parity tolerance"): the reference numbers are fp32 on
-the same (fp32) weights; our weights are stored bf16 and every activation is bf16 with f32
-accumulation, so the bar is relative-L2 <= 3e-2 on logits of attended positions, |dloss| <= 3e-2,
-and relative-L2 <= 6e-2 on the sampled parameter gradients / gradient norms.
+Gates (SURVEY.md §7 "Parity tolerance", bf16 production mode):
+* vs the bf16-faithful oracle on the same weights/inputs: logits rel-L2 <= 1e-2 on attended
+  positions, |dloss| <= 1e-2, every trainable parameter's gradient rel-L2 <= 2e-2;
+* vs the reference's fp32 golden (cross-precision: the bf16-faithful oracle itself sits at
+  logits 1.06e-2 from it, tools/bf16_noise_floor.py): logits <= 2e-2, |dloss| <= 1e-2,
+  gradient norms within 3e-2.
+The f32 parity mode is gated at the north star's 1e-3 in tests/test_parity_modes.py.
 """
 import os
 
@@ -37,16 +42,61 @@ def inputs(seed=2, batch=2, text_len=40, image_col=4, pad_tail=None):
     return ids.cuda(), mask.cuda(), pix.cuda(), labels.cuda()
 
 
+def oracle_bf16(seed, ids, mask, pix, labels):
+    """bf16-faithful oracle forward + backward: (loss, logits, aux, {key: grad})"""
+    cfg = O.config_small_gpu()
+    Wb = {k: v.requires_grad_(True) for k, v in O.to_bf16(O.make_weights(cfg, seed)).items()}
+    cpu = [t.cpu() if t is not None else None for t in (ids, mask, pix, labels)]
+    loss, logits, aux = O.forward(Wb, cfg, cpu[0], cpu[2], cpu[1], cpu[3])
+    loss.backward()
+    return loss, logits, aux, {k: v.grad for k, v in Wb.items()}
+
+
+def check_grads(m, ref_grads, tol=2e-2, arenas=None):
+    """every trainable parameter's gradient vs the oracle's (rel-L2); returns the worst error"""
+    worst, n = 0.0, 0
+    for name, ar in m.arenas.items():
+        if not ar.trainable or (arenas is not None and name not in arenas):
+            continue
+        for k, p in ar.params.items():
+            ref = ref_grads.get(k)
+            if ref is None or float(ref.float().norm()) == 0.0:
+                assert p.grad is None or float(p.grad.float().abs().max()) == 0.0, k
+                continue
+            err = rel_l2(p.grad, ref)
+            worst = max(worst, err)
+            assert err <= tol, (k, err)
+            n += 1
+    assert n > 0
+    return worst
+
+
+def test_forward_backward_matches_bf16_oracle():
+    m = build()
+    ids, mask, pix, labels = inputs()
+    out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
+    loss_ref, logits_ref, aux, grads = oracle_bf16(2, ids, mask, pix, labels)
+    valid = aux["attention_mask"].bool()
+    err = rel_l2(out.logits.float().cpu()[valid], logits_ref.float()[valid])
+    assert err <= 1e-2, err
+    assert abs(out.loss.item() - loss_ref.item()) <= 1e-2, (out.loss.item(), loss_ref.item())
+    out.loss.backward()
+    worst = check_grads(m, grads)
+    print(f"bf16 vs bf16-faithful oracle: logits {err:.2e}, dloss {abs(out.loss.item() - loss_ref.item()):.2e}, "
+          f"worst grad {worst:.2e}")
+
+
 def test_forward_backward_matches_reference_golden():
+    """cross-precision: bf16 production path vs the reference's own fp32 forward/backward"""
     g = np.load(os.path.join(GOLD, "small_gpu.npz"))
     m = build()
     ids, mask, pix, labels = inputs()
     out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
     assert tuple(out.logits.shape) == tuple(g["logits_shape"])
-    assert abs(out.loss.item() - float(g["loss"][0])) <= 3e-2, (out.loss.item(), float(g["loss"][0]))
+    assert abs(out.loss.item() - float(g["loss"][0])) <= 1e-2, (out.loss.item(), float(g["loss"][0]))
     rows = torch.as_tensor(g["logits_rows"])
     sample = out.logits.detach()[:, rows].float().cpu().numpy()
-    assert rel_l2(sample, g["logits_sample"]) <= 3e-2
+    assert rel_l2(sample, g["logits_sample"]) <= 2e-2
     out.loss.backward()
     params = {}
     for ar in m.arenas.values():
@@ -60,27 +110,22 @@ def test_forward_backward_matches_reference_golden():
             if not p.requires_grad:
                 continue  # vision tower frozen in the "full" policy
             ours = p.grad.float().norm().item()
-            assert abs(ours - ref) <= 6e-2 * ref + 1e-6, (k, ours, ref)
+            assert abs(ours - ref) <= 3e-2 * ref + 1e-6, (k, ours, ref)
             checked += 1
-        if key.startswith("grad/"):
-            k = key[len("grad/"):]
-            stride = int(g["gradstride/" + k][0])
-            ours = params[k].grad.float().reshape(-1)[::stride].cpu().numpy()
-            assert rel_l2(ours, g[key]) <= 6e-2, k
     assert checked > 10
 
 
 def test_right_padded_batch_matches_oracle():
-    cfg = O.config_small_gpu()
-    W = O.make_weights(cfg, 3)
-    ids, mask, pix, labels = O.make_inputs(cfg, 2, 48, 3, 3, pad_tail=[0, 9])
-    loss_ref, logits_ref, aux = O.forward(W, cfg, ids, pix, mask, labels)
+    ids, mask, pix, labels = (t.cuda() for t in O.make_inputs(O.config_small_gpu(), 2, 48, 3, 3, pad_tail=[0, 9]))
+    loss_ref, logits_ref, aux, grads = oracle_bf16(3, ids, mask, pix, labels)
     m = build(seed=3)
-    out = m(input_ids=ids.cuda(), pixel_values=pix.cuda(), attention_mask=mask.cuda(), labels=labels.cuda())
+    out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
     valid = aux["attention_mask"].bool()
     ours = out.logits.detach().float().cpu()[valid]
-    assert rel_l2(ours, logits_ref.detach()[valid]) <= 3e-2
-    assert abs(out.loss.item() - loss_ref.item()) <= 3e-2
+    assert rel_l2(ours, logits_ref.detach().float()[valid]) <= 1e-2
+    assert abs(out.loss.item() - loss_ref.item()) <= 1e-2
+    out.loss.backward()
+    check_grads(m, grads)
 
 
 def test_return_dict_false_and_select_strategy_error():
@@ -100,18 +145,16 @@ def test_reference_trainable_policy_grads():
     ids, mask, pix, labels = inputs()
     out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels)
     out.loss.backward()
-    g = np.load(os.path.join(GOLD, "small_gpu.npz"))
-    for k in ["multi_modal_projector.linear_1.weight", "language_model.lm_head.weight",
-              "language_model.model.embed_tokens.weight"]:
-        p = m.arenas["projector" if "projector" in k else ("head" if "lm_head" in k else "embed")].params[k]
-        ref = float(g["gradnorm/" + k][0])
-        assert abs(p.grad.float().norm().item() - ref) <= 6e-2 * ref
+    _, _, _, grads = oracle_bf16(2, ids, mask, pix, labels)
+    check_grads(m, grads)
+    assert {n for n, a in m.arenas.items() if a.trainable} == {"projector", "head", "embed"}
     assert not m.arenas["layers"].trainable
 
 
 def test_full_size_layer_shapes_run():
-    """one full-width Vicuna-7B decoder layer and one CLIP-L layer (B=1) fwd+bwd: shapes,
-    finiteness and fwd parity vs the oracle on the same weights."""
+    """one full-width Vicuna-7B decoder layer and one CLIP-L layer (B=1) through the whole model
+    at config-3 shapes (L = 1088, vocab 32064) fwd+bwd: output shapes, finite loss and non-zero
+    finite gradients. Numerical parity at these widths is tests/test_full_size.py's."""
     from cullavo_amd.config import CuLLaVOConfig, CLIPVisionConfig, LlamaConfig
     from cullavo_amd.arch_cullavo import CuLLaVOModel
     cfg = CuLLaVOConfig(vision_config=CLIPVisionConfig(num_hidden_layers=2),
