@@ -213,7 +213,12 @@ class CuLLaVOModel(nn.Module):
     # -- KV-cache inference (reference :605-636 and HF generate; generation.py) ------------------
     def _forward_cached(self, input_ids, pixel_values, attention_mask, position_ids, cache, inputs_embeds,
                         vision_feature_layer, strategy, labels, return_dict, max_len: int | None = None):
-        from .generation import lm_infer
+        from .generation import KVCache, lm_infer
+        if cache is not None and not isinstance(cache, KVCache):
+            # transformers-layout cache (legacy tuple / DynamicCache, as the reference's decode branch
+            # receives it, arch_cullavo.py:605-636): copied once; the KVCache returned in
+            # past_key_values indexes like the legacy tuple (cache[layer] -> (key, value) [B,H,L,D])
+            cache = KVCache.from_legacy(cache, attention_mask)
         if torch.is_grad_enabled() and any(p.requires_grad for ar in self.arenas.values() for p in ar.params.values()):
             torch.set_grad_enabled(False)  # inference only, as under the reference's torch.inference_mode()
             try:

@@ -47,6 +47,63 @@ class KVCache:
     def get_seq_length(self) -> int:
         return self.length
 
+    def to_legacy_cache(self):
+        """transformers' legacy tuple: ((key, value) [B, H, L, D] per layer), views of this cache"""
+        return tuple(self[i] for i in range(len(self)))
+
+    def grow(self, max_len: int):
+        """re-allocate with room for max_len rows per sequence, keeping the filled rows"""
+        if max_len <= self.max_len:
+            return
+        k = torch.empty((self.k.shape[0], self.B, max_len, self.k.shape[3]), dtype=self.k.dtype, device=self.k.device)
+        v = torch.empty_like(k)
+        k[:, :, :self.length].copy_(self.k[:, :, :self.length])
+        v[:, :, :self.length].copy_(self.v[:, :, :self.length])
+        self.k, self.v, self.max_len = k, v, max_len
+
+    @classmethod
+    def from_legacy(cls, legacy, attention_mask=None, extra: int = 256):
+        """A transformers-layout cache -- the legacy tuple of per-layer (key, value) [B, H, L, D]
+        (what the reference's decode branch indexes, arch_cullavo.py:608-614) or any object with
+        to_legacy_cache() (DynamicCache) -- copied into a KVCache with `extra` free rows.
+        Attended keys: the reference's rule (:611-632) -- a cached position whose first-layer
+        keys are zero is not attended, nor are the
+        left-padding positions of the caller's attention_mask -- which must leave one contiguous
+        span per sequence (what the decode kernels read)."""
+        if hasattr(legacy, "to_legacy_cache"):
+            legacy = legacy.to_legacy_cache()
+        if not isinstance(legacy, (tuple, list)) or not legacy or len(legacy[0]) != 2:
+            raise TypeError(f"past_key_values: expected a KVCache or a transformers legacy cache (tuple of per-layer "
+                            f"(key, value) [B, H, L, D]), got {type(legacy).__name__}")
+        k0 = legacy[0][0]
+        B, H, L, D = k0.shape
+        cache = cls(len(legacy), B, L + extra, H, D, k0.device, dtype=k0.dtype)
+        for i, (k, v) in enumerate(legacy):
+            if k.shape != (B, H, L, D) or v.shape != (B, H, L, D):
+                raise ValueError(f"layer {i}: key {tuple(k.shape)} / value {tuple(v.shape)} vs {(B, H, L, D)}")
+            cache.k[i, :, :L].copy_(k.transpose(1, 2).reshape(B, L, H * D))
+            cache.v[i, :, :L].copy_(v.transpose(1, 2).reshape(B, L, H * D))
+        # a slot is unattended when its first-layer keys are all zero: the reference tests only the
+        # head-dim component 0 summed over the heads, which a real key also hits by chance (two
+        # bf16 values of opposite sign over 2 heads: seen in the tiny config), so every component
+        # is required to vanish here
+        att = k0.float().abs().sum((1, 3)) != 0
+        if attention_mask is not None:
+            if attention_mask.shape[1] >= L:  # a mask over the merged rows
+                att &= attention_mask[:, :L].to(k0.device) != 0
+            else:  # the caller's text-level mask (:618-632): its leading zeros are the left padding
+                lead = (attention_mask.to(torch.int64).cumsum(-1) == 0).sum(-1).to(k0.device)
+                att &= torch.arange(L, device=k0.device)[None] >= lead[:, None]
+        am = att.to(torch.int64)
+        first = (am.cumsum(-1) == 0).sum(-1)
+        if bool((am.sum(-1) + first != L).any()):
+            raise NotImplementedError("KV-cache decode needs one contiguous attended span per sequence "
+                                      "(left padding only)")
+        cache.length = L
+        cache.kv_start = first.to(torch.int32)
+        cache.next_pos = am.sum(-1)
+        return cache
+
 
 def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int, start, kv_len):
     """One LlamaDecoderLayer over Lnew new rows per sequence (prefill: Lnew = prompt length on an
@@ -105,8 +162,8 @@ def lm_infer(lm, embeds, attention_mask, position_ids, cache: KVCache | None, ma
     else:
         if Lnew != 1:
             raise NotImplementedError("after the prefill, cached steps take one token per sequence")
-        if cache.length + 1 > cache.max_len:
-            raise ValueError(f"KV cache full ({cache.max_len} rows)")
+        if cache.length + 1 > cache.max_len:  # room for 256 more steps (one copy per 256 steps)
+            cache.grow(cache.max_len + 256)
         if position_ids is None:
             position_ids = cache.next_pos[:, None]
         cache.next_pos = cache.next_pos + 1

@@ -156,3 +156,34 @@ def test_left_padded_batch_matches_single():
     two = m.generate(input_ids=batch_ids.cuda(), pixel_values=batch_pix.cuda(), attention_mask=batch_mask.cuda(),
                      max_new_tokens=4)
     assert torch.equal(two[0, 25:].cpu(), one[0, 20:].cpu())
+
+
+@pytest.mark.gpu
+def test_transformers_layout_cache_decode_matches_kvcache():
+    """A decode step fed a transformers-layout cache (the legacy tuple of per-layer (key, value)
+    [B, H, L, D] that the reference's decode branch indexes, arch_cullavo.py:605-636) with the
+    caller's text-level attention_mask (left padding in row 0) gives bitwise the logits of the
+    same step on the native KVCache, and the returned cache indexes like the legacy tuple."""
+    from cullavo_amd.generation import KVCache
+    cfg = O.config_small_gpu()
+    m = _model(6)
+    ids, mask, pix, _ = O.make_inputs(cfg, 2, 20, 3, 17)
+    pad = cfg.pad_token_id
+    ids = torch.cat([torch.full((2, 4), pad), ids], 1)
+    ids[1, :4] = torch.randint(2, cfg.image_token_index, (4,), generator=torch.Generator().manual_seed(3))
+    mask = torch.cat([torch.ones(2, 4, dtype=mask.dtype), mask], 1)
+    mask[0, :4] = 0
+    ids, mask, pix = ids.cuda(), mask.cuda(), pix.cuda()
+    out = m(input_ids=ids, pixel_values=pix, attention_mask=mask, use_cache=True)
+    native = out.past_key_values
+    legacy = tuple((k.clone(), v.clone()) for k, v in native.to_legacy_cache())
+    tok = torch.randint(2, cfg.image_token_index, (2, 1), generator=torch.Generator().manual_seed(4)).cuda()
+    step_mask = torch.cat([mask, torch.ones(2, 1, dtype=mask.dtype, device=mask.device)], 1)
+    a = m(input_ids=tok, past_key_values=legacy, attention_mask=step_mask, use_cache=True)
+    b = m(input_ids=tok, past_key_values=native, attention_mask=step_mask, use_cache=True)
+    assert torch.equal(a.logits, b.logits)
+    assert isinstance(a.past_key_values, KVCache)
+    first = a.past_key_values[0][0][:, :, :, 0]  # the reference's indexing (:611)
+    assert first.shape == (2, cfg.text.num_attention_heads, native.get_seq_length())
+    with pytest.raises(TypeError, match="legacy cache"):
+        m(input_ids=tok, past_key_values=torch.zeros(3), attention_mask=step_mask, use_cache=True)

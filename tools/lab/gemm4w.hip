@@ -1,0 +1,242 @@
+// GEMM lab, round 3: the 256x256 tile with FOUR waves (one per SIMD), each owning a 128x128 output
+// block (8 x 8 MFMA 16x16x32 tiles, 256 accumulator registers) -- the geometry of the hipBLASLt
+// kernel that beats the production 8-wave kernel on the forward shapes
+// (Cijk_..._MT256x256x32_MI16x16x1_..._MIWT8_8_..._WG32_8_1, profiles/r02). Forward layout only:
+// C[M][N] = A[M][K] . B[N][K]^T, bf16 in, f32 accumulate, bf16 out; K % 32 == 0.
+//
+//   hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/lab/gemm4w.hip -o tools/lab/libgemm4w.so
+//   python tools/lab/gemm_lab.py --lib tools/lab/libgemm4w.so --variants 0,1 --shapes gate_up,lm_head,o
+//
+// BK = 32, three LDS stages of [256 rows][32 k] per operand (96 KiB), one barrier per K-tile.
+// Step kt computes K-tile kt from fragments already in registers while it reads tile kt+1's
+// fragments (registers of the other fragment set), writes or DMAs a later tile into the stage
+// nobody reads, and issues the global loads of the tile after that.
+//   variant 0: register staging (buffer_load_dwordx4 -> VGPR, ds_write_b128 one step later)
+//   variants 1/2/3: LDS-DMA staging (buffer_load ... lds, counted vmcnt before the barrier) into
+//   3/4/5 stages (tile kt+S issued at step kt: S-1 steps of latency budget)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short u16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 frag8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+#define DEV __device__ __forceinline__
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int OPB = 256 * BK * 2;  // 16 KiB per operand tile
+constexpr int STAGE = 2 * OPB;
+constexpr unsigned kOOB = 0x7FFFFFF0u;
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int kLgkm0 = 0xC07F;  // lgkmcnt(0)
+constexpr int kVm8 = 0x0F78;    // vmcnt(8)
+constexpr int kVm0 = 0x0F70;    // vmcnt(0)
+
+// [256 rows][32 k] image, 64-B rows of four 16-B chunks; chunk c of row r sits in slot
+// c ^ (3 * ((r >> 3) & 1)): conflict-free for ds_read_b128 fragment reads (lane l: row l & 15,
+// chunk l >> 4) and for the staging writes (lanes 4r..4r+3: one row)
+DEV int img(int row, int c) { return row * 64 + ((c ^ (((row >> 3) & 1) * 3)) << 4); }
+
+DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+DEV __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+struct Frags {
+  frag8 a[8], b[8];
+};
+
+// wait until at most n of this wave's LDS-DMA K-tiles (8 pieces each) are still in flight
+DEV void wait_tiles(int n) {
+  if (n <= 0) __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
+  else if (n == 1) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+  else if (n == 2) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+  else __builtin_amdgcn_s_waitcnt(0x4F78);              // vmcnt(24)
+}
+
+template <int V, int S>
+__global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u16* __restrict__ B,
+                                              u16* __restrict__ C, int M, int N, int K, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nwg = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, nwg);
+  // groups of 4 N-tiles sweeping the M-tiles
+  const int per_group = 4 * tiles_m;
+  const int group = lid / per_group;
+  const int first_n = group * 4;
+  const int gsize = min(tiles_n - first_n, 4);
+  const int n0 = (first_n + (lid % per_group) % gsize) * 256;
+  const int m0 = ((lid % per_group) / gsize) * 256;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(A, (int64_t)M * K * 2);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(B, (int64_t)N * K * 2);
+  const int nk = K / BK;
+
+  // staging geometry
+  unsigned offA[4], offB[4];
+  int lds_w[4];
+  if constexpr (V == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (t >> 2) + 64 * i, c = t & 3;
+      offA[i] = m0 + row < M ? (unsigned)(((int64_t)(m0 + row) * K + c * 8) * 2) : kOOB;
+      offB[i] = n0 + row < N ? (unsigned)(((int64_t)(n0 + row) * K + c * 8) * 2) : kOOB;
+      lds_w[i] = img(row, c);
+    }
+  } else {
+    // pieces wave + 4i (i = 0..3) of each operand: piece p = rows 16p..16p+15, lane l -> row
+    // 16p + (l >> 2), slot l & 3 holding chunk (l & 3) ^ swz(row)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = wave + 4 * i;
+      const int row = 16 * p + (lane >> 2);
+      const int c = (lane & 3) ^ (((row >> 3) & 1) * 3);
+      offA[i] = m0 + row < M ? (unsigned)(((int64_t)(m0 + row) * K + c * 8) * 2) : kOOB;
+      offB[i] = n0 + row < N ? (unsigned)(((int64_t)(n0 + row) * K + c * 8) * 2) : kOOB;
+      lds_w[i] = p * 1024;
+    }
+  }
+  u32x4 st[8];
+  auto gload = [&](int kt) {
+    const int so = kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      st[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, offA[i], so, 0);
+      st[4 + i] = __builtin_amdgcn_raw_buffer_load_b128(rb, offB[i], so, 0);
+    }
+  };
+  auto swrite = [&](int kt) {
+    char* s = smem + (kt % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<u32x4*>(s + lds_w[i]) = st[i];
+      *reinterpret_cast<u32x4*>(s + OPB + lds_w[i]) = st[4 + i];
+    }
+  };
+  auto dma = [&](int kt) {
+    char* s = smem + (kt % S) * STAGE;
+    const int so = kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(s + lds_w[i]), 16, offA[i], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(s + OPB + lds_w[i]), 16, offB[i], so, 0, 0);
+    }
+  };
+  const int ra_row = wr * 128 + (lane & 15), rb_row = wc * 128 + (lane & 15), ch = lane >> 4;
+  auto fread = [&](int kt, Frags& f) {
+    const char* s = smem + (kt % S) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.a[i] = *reinterpret_cast<const frag8*>(s + img(ra_row + i * 16, ch));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.b[j] = *reinterpret_cast<const frag8*>(s + OPB + img(rb_row + j * 16, ch));
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tiles 0 and 1 resident, tile 2 on its way
+  if constexpr (V == 0) {
+    gload(0);
+    swrite(0);
+    if (nk > 1) { gload(1); swrite(1); }
+    if (nk > 2) gload(2);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+  } else {
+    // tiles 0 .. S-1 issued; tiles 0 and 1 must have landed
+#pragma unroll
+    for (int u = 0; u < S; ++u)
+      if (u < nk) dma(u);
+    wait_tiles(min(S, nk) - 2);
+  }
+  __builtin_amdgcn_s_barrier();
+  Frags F0, F1;
+  fread(0, F0);
+  __builtin_amdgcn_s_waitcnt(kLgkm0);  // loop entry with no LDS op in flight (else the waitcnt
+                                       // pass puts lgkmcnt(0) before every step's first MFMA)
+
+  auto step = [&](int kt, Frags& cur, Frags& nxt) {
+    if (kt + 1 < nk) fread(kt + 1, nxt);
+    if constexpr (V == 0) {
+      if (kt + 2 < nk) swrite(kt + 2);
+      if (kt + 3 < nk) gload(kt + 3);
+    } else {
+      if (kt + S < nk) dma(kt + S);  // into tile kt's stage: its fragments were read last step
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[j], cur.a[i], acc[i][j], 0, 0, 0);
+    // keep the MFMAs on this side of the wait and the barrier (hipcc moves register-only MFMAs
+    // across inline-asm waits, cdna_hip_programming.md rule 18): the LDS traffic issued above
+    // runs under them
+    __builtin_amdgcn_sched_barrier(0);
+    // waits through the builtin, not inline asm: the compiler's waitcnt pass then knows the
+    // fragments read above are retired and puts no lgkmcnt(0) in front of the next step's MFMAs
+    if constexpr (V == 1) {
+      // tile kt + 2 (read next step) must have landed before this barrier; the newer ones fly
+      wait_tiles(min(kt + S, nk - 1) - (kt + 2));
+    }
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, F0, F1);
+    step(kt + 1, F1, F0);
+  }
+  if (kt < nk) step(kt, F0, F1);
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wc * 128 + j * 16 + 4 * (lane >> 4);
+      if (n >= N) continue;
+      const bf16x4 v = __builtin_convertvector(acc[i][j], bf16x4);
+      *reinterpret_cast<bf16x4*>(C + (int64_t)m * N + n) = v;
+    }
+  }
+}
+
+template <int V, int S>
+int launch(int M, int N, int K, const void* A, const void* B, void* C, hipStream_t s) {
+  const int smem = S * STAGE;
+  static bool set = false;
+  if (!set) {
+    (void)hipFuncSetAttribute((const void*)g4w<V, S>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    set = true;
+  }
+  const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+  g4w<V, S><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // namespace
+
+extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, const void* B, void* C, void* stream) {
+  if (K % BK) return 2;
+  hipStream_t s = (hipStream_t)stream;
+  switch (v) {
+    case 0: return launch<0, 3>((int)M, (int)N, (int)K, A, B, C, s);
+    case 1: return launch<1, 3>((int)M, (int)N, (int)K, A, B, C, s);
+    case 2: return launch<1, 4>((int)M, (int)N, (int)K, A, B, C, s);
+    case 3: return launch<1, 5>((int)M, (int)N, (int)K, A, B, C, s);
+  }
+  return 3;
+}

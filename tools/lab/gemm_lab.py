@@ -22,7 +22,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--lib", default=os.path.join(HERE, "libgemm_lab.so"))
+    ap.add_argument("--prod", action="store_true", help="also time the production kernel (cullavo_amd.ops.linear)")
     a = ap.parse_args()
+    prod = None
+    if a.prod:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        from cullavo_amd import ops as prod
     lib = ctypes.CDLL(a.lib)
     lib.lab_gemm.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -44,8 +50,20 @@ def main():
             assert rc == 0, (v, rc)
             torch.cuda.synchronize()
             errs[v] = ((C.float() - ref).norm() / ref.norm()).item()
-        tb = []
+        tb, tp = [], []
+        if prod is not None:
+            yp = prod.linear(A, B)
+            torch.cuda.synchronize()
+            errs["prod"] = ((yp.float() - ref).norm() / ref.norm()).item()
         for _ in range(a.rounds):
+            if prod is not None:
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(a.iters):
+                    prod.linear(A, B, out=yp)
+                e.record()
+                e.synchronize()
+                tp.append(fl / (s.elapsed_time(e) / a.iters) / 1e9)
             for v in variants:
                 lib.lab_gemm(v, M, N, K, A.data_ptr(), B.data_ptr(), C.data_ptr(), stream)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -63,6 +81,8 @@ def main():
             e.synchronize()
             tb.append(fl / (s.elapsed_time(e) / a.iters) / 1e9)
         line = f"{name:8s} M={M} N={N} K={K} hipBLASLt {statistics.median(tb):7.1f}"
+        if tp:
+            line += f" | prod {statistics.median(tp):7.1f} (err {errs['prod']:.1e})"
         for v in variants:
             line += f" | v{v} {statistics.median(res[v]):7.1f} (err {errs[v]:.1e})"
         print(line, flush=True)
