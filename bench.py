@@ -10,6 +10,12 @@ layers, lm_head + shifted masked CE, the complete backward, bucketed RCCL gradie
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+At N = 1 the default run also times the other BASELINE workloads, each in a child process started
+before this process touches the GPU (so their memory never overlaps): config 2 (CLIP ViT-L/14-336
+encoder, bs 64), config 5 (ViT-L + Llama-2-13B, L = 1600, bs 4) and the reference's own recipe on
+config 3 (LoRA r=64 + projector / lm_head / embed, frozen base). They are reported under
+"workloads", each with its own roofline object; the headline (metric / value) stays config 3.
+
 Prints ONE JSON line on rank 0 (see README / DESIGN.md §Measurement for every field).
 """
 from __future__ import annotations
@@ -46,7 +52,51 @@ def parse():
     ap.add_argument("--workload", default="step", choices=["step", "vit"],
                     help="step: the training step (default; configs 3/4/5 by --config/--batch/--text-len); "
                          "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64)")
+    ap.add_argument("--sub-workloads", default=",".join(SUB_WORKLOADS),
+                    help="N=1 headline runs only: the other workloads timed in child processes ('' = none)")
+    ap.add_argument("--no-sub", action="store_true", help="time this workload only")
     return ap.parse_args()
+
+
+# the other BASELINE workloads a default N = 1 run reports beside the config-3 headline
+SUB_WORKLOADS = {
+    "config2-vit": ["--workload", "vit", "--batch", "64"],
+    "config5-full": ["--config", "llava-1.5-13b", "--batch", "4", "--text-len", "1025"],
+    "config3-lora": ["--trainable", "lora"],
+}
+
+
+def workload_key(args) -> str:
+    """the key PMC records are filed under (profiles/roofline_traffic.json)"""
+    if args.workload == "vit":
+        return "config2-vit"
+    return f"{'config5' if '13b' in args.config else 'config3'}-{args.trainable}"
+
+
+def run_sub_workloads(args, names):
+    """Each workload in its own child process (sequentially, before this process initialises the
+    GPU), its one JSON line parsed and condensed; a failing child is reported, not fatal."""
+    import subprocess
+    out = {}
+    for name in names:
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-sub", "--no-cpu-baseline",
+               "--steps", str(min(args.steps, 10)), "--warmup", str(min(args.warmup, 3)), *SUB_WORKLOADS[name]]
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out[name] = {"error": f"rc {r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
+                continue
+            rec = json.loads(lines[-1])
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": "timed out after 600 s"}
+            continue
+        keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops_per_gpu", "mfu",
+                "gflop_per_image", "loss", "roofline", "gemm_kernels")
+        out[name] = {k: rec[k] for k in keep if k in rec}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+    return out
 
 
 
@@ -102,6 +152,7 @@ def vit_main(args):
     tf = fl_img * args.batch / (elapsed / args.steps) / 1e12
     top = fams[0]
     if rank == 0:
+        traffic, mfma_busy = measured_traffic(top["kernel"], workload_key(args))
         line = {
             "metric": "CLIP ViT-L/14-336 encoder images/sec (forward, hidden_states[-2])",
             "value": round(imgs / elapsed, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -113,11 +164,16 @@ def vit_main(args):
                        "model": "clip-vit-large-patch14-336", "global_batch": world * args.batch, "seq_len": 577,
                        "parallelism": f"dp{world}"},
             "model_tflops_per_gpu": round(tf, 2), "gflop_per_image": round(fl_img / 1e9, 1),
-            "roofline": {"kernel": f"whole encoder (dominant kernel {top['kernel']}, {top['role']}: "
-                                   f"{100 * top['ms'] / (elapsed * 1e3):.1f} % of the time at "
-                                   f"{top['achieved_tflops']:.0f} TFLOP/s)",
-                         "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tf / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "roofline": {"kernel": f"{top['kernel']}: {top['role']}, {len(top['shapes'])} shapes "
+                                   f"{['x'.join(map(str, sh)) for sh in top['shapes']]} (M x N x K), "
+                                   f"{top['launches'] // args.steps} launches/step, "
+                                   f"{100 * top['ms'] / (elapsed * 1e3):.1f} % of the encoder time",
+                         "bound": "mfma", "achieved": round(top["achieved_tflops"], 2), "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(top["achieved_tflops"] / PEAK_BF16_TFLOPS, 4),
+                         "traffic": traffic, "mfma_busy": mfma_busy,
+                         "algorithmic_bytes": round(top["bytes"] / top["launches"]),
+                         "avg_ms": round(top["ms"] / top["launches"], 4),
+                         "encoder_frac": round(tf / PEAK_BF16_TFLOPS, 4),
                          "library_ceiling": gemm_ceiling(top) if world == 1 else None},
             "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share": round(f["ms"] / (elapsed * 1e3), 4),
                               "achieved_tflops": round(f["achieved_tflops"], 1)} for f in fams[:4]],
@@ -246,17 +302,18 @@ def gemm_families(launches):
     return out
 
 
-def measured_traffic(kname):
+def measured_traffic(kname, workload):
     """HBM bytes per launch of the roofline kernel (average over its launches in one profiled
-    step) and its MFMA busy fraction, from the committed PMC passes (None if the profile was
-    taken on another kernel)."""
+    step) and its MFMA busy fraction, from the committed PMC passes of THIS workload (records
+    keyed by workload and kernel; None when no pass was taken on that pair)."""
     path = os.path.join(REPO, "profiles", "roofline_traffic.json")
     try:
-        rec = json.load(open(path))
+        recs = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    if rec.get("kernel") == kname:
-        return rec.get("bytes_per_launch"), rec.get("mfma_busy_frac")
+    for rec in recs.get("records", []):
+        if rec.get("kernel") == kname and rec.get("workload") == workload:
+            return rec.get("bytes_per_launch"), rec.get("mfma_busy_frac")
     return None, None
 
 
@@ -299,6 +356,11 @@ def gemm_ceiling(fam, iters=10):
 
 def main():
     args = parse()
+    subs = None
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    names = [n for n in args.sub_workloads.split(",") if n]
+    if world == 1 and not args.no_sub and args.workload == "step" and names:
+        subs = run_sub_workloads(args, names)  # before this process touches the GPU
     if args.workload == "vit":
         if args.batch == 8:
             args.batch = 64  # BASELINE config 2
@@ -309,7 +371,6 @@ def main():
     from cullavo_amd import ops
     from cullavo_amd.trainer import CuLLaVO_Trainer
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     opt = {"MODEL": {"CONFIG": args.config}, "LLM": {"TRAINABLE": args.trainable},
@@ -371,7 +432,7 @@ def main():
     step_tflops = fl["train"] * world * args.batch / (elapsed / args.steps) / 1e12
     top = fams[0]
     kname = top["kernel"]
-    traffic, mfma_busy = measured_traffic(kname)
+    traffic, mfma_busy = measured_traffic(kname, workload_key(args))
     achieved = top["achieved_tflops"]
     n_launch = top["launches"]
     if rank == 0:
@@ -409,8 +470,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                 "traffic": traffic,
-                "traffic_unit": "bytes/launch averaged over the kernel's launches in one step (HBM, rocprofv3 "
-                                "FETCH_SIZE x2 + WRITE_SIZE; profiles/roofline_traffic.json)" if traffic else None,
+                "traffic_unit": "bytes/launch averaged over the kernel's launches in one step of this workload (HBM, "
+                                "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; profiles/roofline_traffic.json)" if traffic else None,
                 "algorithmic_bytes": round(top["bytes"] / n_launch),
                 "mfma_busy": mfma_busy,
                 "avg_ms": round(top["ms"] / n_launch, 4),
@@ -425,6 +486,8 @@ def main():
             line["roofline"]["library_ceiling"] = gemm_ceiling(top)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)
+        if subs is not None:
+            line["workloads"] = subs
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -62,7 +62,10 @@ DEV void wait_tiles(int n) {
   else __builtin_amdgcn_s_waitcnt(0x4F78);              // vmcnt(24)
 }
 
-template <int V, int S>
+// sched_group_barrier masks
+constexpr int kMFMA = 0x008, kDSR = 0x100, kDSW = 0x200, kVMR = 0x020;
+
+template <int V, int S, int IL>
 __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u16* __restrict__ B,
                                               u16* __restrict__ C, int M, int N, int K, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -86,7 +89,7 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   // staging geometry
   unsigned offA[4], offB[4];
   int lds_w[4];
-  if constexpr (V == 0) {
+  if constexpr (V != 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = (t >> 2) + 64 * i, c = t & 3;
@@ -107,8 +110,10 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
       lds_w[i] = p * 1024;
     }
   }
-  u32x4 st[8];
-  auto gload = [&](int kt) {
+  u32x4 st0[8], st1[8];
+  // tiles >= nk read out of range (buffer loads return zeros): the staging ops stay unconditional,
+  // in the MFMAs' basic block, where sched_group_barrier can interleave them
+  auto gload = [&](int kt, u32x4 (&st)[8]) {
     const int so = kt * BK * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
       st[4 + i] = __builtin_amdgcn_raw_buffer_load_b128(rb, offB[i], so, 0);
     }
   };
-  auto swrite = [&](int kt) {
+  auto swrite = [&](int kt, const u32x4 (&st)[8]) {
     char* s = smem + (kt % S) * STAGE;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -148,12 +153,21 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: tiles 0 and 1 resident, tile 2 on its way
+  // prologue: tiles 0 and 1 resident, the next ones on their way
   if constexpr (V == 0) {
-    gload(0);
-    swrite(0);
-    if (nk > 1) { gload(1); swrite(1); }
-    if (nk > 2) gload(2);
+    gload(0, st0);
+    swrite(0, st0);
+    gload(1, st0);
+    swrite(1, st0);
+    gload(2, st0);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+  } else if constexpr (V == 2) {
+    gload(0, st0);
+    swrite(0, st0);
+    gload(1, st1);
+    swrite(1, st1);
+    gload(2, st0);
+    gload(3, st1);
     __builtin_amdgcn_s_waitcnt(kLgkm0);
   } else {
     // tiles 0 .. S-1 issued; tiles 0 and 1 must have landed
@@ -168,18 +182,41 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   __builtin_amdgcn_s_waitcnt(kLgkm0);  // loop entry with no LDS op in flight (else the waitcnt
                                        // pass puts lgkmcnt(0) before every step's first MFMA)
 
-  auto step = [&](int kt, Frags& cur, Frags& nxt) {
-    if (kt + 1 < nk) fread(kt + 1, nxt);
+  // step kt: MFMAs on tile kt (fragments in cur) with, under them, tile kt+1's fragment reads
+  // into nxt and the staging of a later tile. P = kt & 1 (the 2-deep register staging's set).
+  auto step = [&](int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
+    fread(kt + 1 < nk ? kt + 1 : kt, nxt);
     if constexpr (V == 0) {
-      if (kt + 2 < nk) swrite(kt + 2);
-      if (kt + 3 < nk) gload(kt + 3);
+      swrite(kt + 2, st0);  // loaded last step (1 step of latency)
+      gload(kt + 3, st0);
+    } else if constexpr (V == 2) {
+      swrite(kt + 2, stp);  // loaded two steps ago
+      gload(kt + 4, stp);
     } else {
-      if (kt + S < nk) dma(kt + S);  // into tile kt's stage: its fragments were read last step
+      dma(kt + S);  // into tile kt's stage: its fragments were read last step
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[j], cur.a[i], acc[i][j], 0, 0, 0);
+    if constexpr (IL) {
+      // one memory op per MFMA gap: the wave (alone on its SIMD) issues them while the previous
+      // MFMA occupies the matrix pipe, instead of in a burst with the pipe idle
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kDSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kDSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
+        if constexpr (V != 1) {
+          __builtin_amdgcn_sched_group_barrier(kDSW, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(kMFMA, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(kVMR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kMFMA, V != 1 ? 4 : 5, 0);
+      }
+    }
     // keep the MFMAs on this side of the wait and the barrier (hipcc moves register-only MFMAs
     // across inline-asm waits, cdna_hip_programming.md rule 18): the LDS traffic issued above
     // runs under them
@@ -188,17 +225,17 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
     // fragments read above are retired and puts no lgkmcnt(0) in front of the next step's MFMAs
     if constexpr (V == 1) {
       // tile kt + 2 (read next step) must have landed before this barrier; the newer ones fly
-      wait_tiles(min(kt + S, nk - 1) - (kt + 2));
+      wait_tiles(S - 2);
     }
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   };
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    step(kt, F0, F1);
-    step(kt + 1, F1, F0);
+    step(kt, F0, F1, st0);
+    step(kt + 1, F1, F0, st1);
   }
-  if (kt < nk) step(kt, F0, F1);
+  if (kt < nk) step(kt, F0, F1, st0);
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -214,16 +251,16 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   }
 }
 
-template <int V, int S>
+template <int V, int S, int IL>
 int launch(int M, int N, int K, const void* A, const void* B, void* C, hipStream_t s) {
   const int smem = S * STAGE;
   static bool set = false;
   if (!set) {
-    (void)hipFuncSetAttribute((const void*)g4w<V, S>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)g4w<V, S, IL>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     set = true;
   }
   const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-  g4w<V, S><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
+  g4w<V, S, IL><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -233,10 +270,14 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
   if (K % BK) return 2;
   hipStream_t s = (hipStream_t)stream;
   switch (v) {
-    case 0: return launch<0, 3>((int)M, (int)N, (int)K, A, B, C, s);
-    case 1: return launch<1, 3>((int)M, (int)N, (int)K, A, B, C, s);
-    case 2: return launch<1, 4>((int)M, (int)N, (int)K, A, B, C, s);
-    case 3: return launch<1, 5>((int)M, (int)N, (int)K, A, B, C, s);
+    case 0: return launch<0, 3, 0>((int)M, (int)N, (int)K, A, B, C, s);
+    case 1: return launch<1, 3, 0>((int)M, (int)N, (int)K, A, B, C, s);
+    case 2: return launch<1, 4, 0>((int)M, (int)N, (int)K, A, B, C, s);
+    case 3: return launch<1, 5, 0>((int)M, (int)N, (int)K, A, B, C, s);
+    case 4: return launch<1, 4, 1>((int)M, (int)N, (int)K, A, B, C, s);  // DMA, interleaved
+    case 5: return launch<2, 3, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep, interleaved
+    case 6: return launch<2, 3, 0>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep
+    case 7: return launch<0, 3, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 1-deep, interleaved
   }
   return 3;
 }

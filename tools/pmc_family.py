@@ -9,7 +9,10 @@ FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
 MFMA busy fraction = (SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs),
 summed over the dispatches (time-weighted).
 
-  python tools/pmc_family.py <fetch.csv> <write.csv> <sq.csv> "<kernel name substring>" > profiles/roofline_traffic.json
+  python tools/pmc_family.py <fetch.csv> <write.csv> <sq.csv> "<kernel name>" <workload key> > record.json
+
+The record (keyed by workload and kernel) goes into profiles/roofline_traffic.json's "records",
+which bench.py reads for the same (workload, kernel) pair only.
 """
 import csv
 import json
@@ -18,6 +21,8 @@ from collections import defaultdict
 
 
 def per_dispatch(path, kname):
+    """counters per dispatch of the kernel whose name (template arguments as rocprofv3 prints
+    them) contains kname"""
     d = defaultdict(dict)
     for r in csv.DictReader(open(path)):
         if kname in r["Kernel_Name"]:
@@ -28,10 +33,11 @@ def per_dispatch(path, kname):
 
 def main():
     fcsv, wcsv, scsv, kname = sys.argv[1:5]
+    workload = sys.argv[5] if len(sys.argv) > 5 else "config3-full"
     f, w, q = per_dispatch(fcsv, kname), per_dispatch(wcsv, kname), per_dispatch(scsv, kname)
     fetch = [v["FETCH_SIZE"] for v in f.values() if "FETCH_SIZE" in v]
     write = [v["WRITE_SIZE"] for v in w.values() if "WRITE_SIZE" in v]
-    out = {"kernel": kname, "dispatches": [len(fetch), len(write), len(q)]}
+    out = {"workload": workload, "kernel": kname, "dispatches": [len(fetch), len(write), len(q)]}
     if fetch and write:
         out["fetch_kib_per_launch_raw"] = sum(fetch) / len(fetch)
         out["write_kib_per_launch"] = sum(write) / len(write)
