@@ -93,7 +93,7 @@ def run_sub_workloads(args, names):
             out[name] = {"error": "timed out after 600 s"}
             continue
         keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops_per_gpu", "mfu",
-                "gflop_per_image", "loss", "roofline", "gemm_kernels")
+                "gflop_per_image", "loss", "roofline", "gemm_kernels", "gemm_shapes")
         out[name] = {k: rec[k] for k in keep if k in rec}
         out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
     return out
@@ -143,7 +143,8 @@ def vit_main(args):
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-    fams = gemm_families(ops.trace_launches())
+    launches = ops.trace_launches()
+    fams = gemm_families(launches)
     if world > 1:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -177,6 +178,7 @@ def vit_main(args):
                          "library_ceiling": gemm_ceiling(top) if world == 1 else None},
             "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share": round(f["ms"] / (elapsed * 1e3), 4),
                               "achieved_tflops": round(f["achieved_tflops"], 1)} for f in fams[:4]],
+            "gemm_shapes": gemm_shapes(launches, args.steps),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -302,6 +304,22 @@ def gemm_families(launches):
     return out
 
 
+def gemm_shapes(launches, steps, top=12):
+    """per-shape GEMM time of the timed steps (the largest first): where each family's time goes"""
+    sh = {}
+    for (M, N, K, al, bl), ms in launches:
+        r = sh.setdefault((M, N, K, al, bl), [0, 0.0])
+        r[0] += 1
+        r[1] += ms
+    out = []
+    for (M, N, K, al, bl), (n, ms) in sorted(sh.items(), key=lambda kv: -kv[1][1])[:top]:
+        name, grid = gemm_kernel_name(M, N, K, al, bl)
+        out.append({"shape": f"{M}x{N}x{K}", "layouts": [al, bl], "kernel": name, "grid": grid,
+                    "launches_per_step": round(n / steps, 2), "ms_per_step": round(ms / steps, 3),
+                    "tflops": round(2.0 * M * N * K * n / (ms * 1e-3) / 1e12, 1)})
+    return out
+
+
 def measured_traffic(kname, workload):
     """HBM bytes per launch of the roofline kernel (average over its launches in one profiled
     step) and its MFMA busy fraction, from the committed PMC passes of THIS workload (records
@@ -417,7 +435,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    fams = gemm_families(ops.trace_launches())
+    launches = ops.trace_launches()
+    fams = gemm_families(launches)
     if world > 1:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -481,6 +500,7 @@ def main():
             "gemm_kernels": [{"kernel": f["kernel"], "role": f["role"], "share_of_step": round(f["ms"] / (elapsed * 1e3), 4),
                               "achieved_tflops": round(f["achieved_tflops"], 1),
                               "frac": round(f["achieved_tflops"] / PEAK_BF16_TFLOPS, 4)} for f in fams[:6]],
+            "gemm_shapes": gemm_shapes(launches, args.steps),
         }
         if world == 1:
             line["roofline"]["library_ceiling"] = gemm_ceiling(top)

@@ -65,7 +65,9 @@ DEV void wait_tiles(int n) {
 // sched_group_barrier masks
 constexpr int kMFMA = 0x008, kDSR = 0x100, kDSW = 0x200, kVMR = 0x020;
 
-template <int V, int S, int IL>
+// AB: ablations (results wrong): 1 = no MFMAs (staging + fragment reads only), 2 = no staging
+// (MFMAs + fragment reads of the prologue tiles only)
+template <int V, int S, int IL, int AB = 0>
 __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u16* __restrict__ B,
                                               u16* __restrict__ C, int M, int N, int K, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -185,8 +187,9 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   // step kt: MFMAs on tile kt (fragments in cur) with, under them, tile kt+1's fragment reads
   // into nxt and the staging of a later tile. P = kt & 1 (the 2-deep register staging's set).
   auto step = [&](int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
-    fread(kt + 1 < nk ? kt + 1 : kt, nxt);
-    if constexpr (V == 0) {
+    fread(AB == 2 ? (kt & 1) : kt + 1 < nk ? kt + 1 : kt, nxt);
+    if constexpr (AB == 2) {
+    } else if constexpr (V == 0) {
       swrite(kt + 2, st0);  // loaded last step (1 step of latency)
       gload(kt + 3, st0);
     } else if constexpr (V == 2) {
@@ -195,10 +198,16 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
     } else {
       dma(kt + S);  // into tile kt's stage: its fragments were read last step
     }
+    if constexpr (AB == 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(cur.a[i]), "v"(cur.b[i]));
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[j], cur.a[i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.b[j], cur.a[i], acc[i][j], 0, 0, 0);
+    }
     if constexpr (IL) {
       // one memory op per MFMA gap: the wave (alone on its SIMD) issues them while the previous
       // MFMA occupies the matrix pipe, instead of in a burst with the pipe idle
@@ -223,7 +232,7 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
     __builtin_amdgcn_sched_barrier(0);
     // waits through the builtin, not inline asm: the compiler's waitcnt pass then knows the
     // fragments read above are retired and puts no lgkmcnt(0) in front of the next step's MFMAs
-    if constexpr (V == 1) {
+    if constexpr (V == 1 && AB != 2) {
       // tile kt + 2 (read next step) must have landed before this barrier; the newer ones fly
       wait_tiles(S - 2);
     }
@@ -251,16 +260,16 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   }
 }
 
-template <int V, int S, int IL>
+template <int V, int S, int IL, int AB = 0>
 int launch(int M, int N, int K, const void* A, const void* B, void* C, hipStream_t s) {
   const int smem = S * STAGE;
   static bool set = false;
   if (!set) {
-    (void)hipFuncSetAttribute((const void*)g4w<V, S, IL>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)g4w<V, S, IL, AB>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     set = true;
   }
   const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-  g4w<V, S, IL><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
+  g4w<V, S, IL, AB><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -278,6 +287,9 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
     case 5: return launch<2, 3, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep, interleaved
     case 6: return launch<2, 3, 0>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep
     case 7: return launch<0, 3, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 1-deep, interleaved
+    case 8: return launch<1, 4, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);   // DMA staging alone (wrong)
+    case 9: return launch<2, 3, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);   // register staging alone (wrong)
+    case 10: return launch<1, 4, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // MFMA + fragment reads alone (wrong)
   }
   return 3;
 }
