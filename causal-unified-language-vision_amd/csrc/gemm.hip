@@ -754,7 +754,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
 
   f32x4 acc[TMW][TN];
-  tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, 0, (int)cdiv(p.K, BK), smem, wave, lane, acc);
+  const int nk_all = (int)cdiv(p.K, BK);
+  if (p.part) {  // split-K (blockIdx.y = split): raw f32 partials, reduced in split order afterwards
+    const int kb = (int)blockIdx.y * p.kt_per;
+    tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, kb, min(nk_all, kb + p.kt_per), smem, wave, lane,
+                                                acc);
+    float* part = p.part + (int64_t)blockIdx.y * p.M * p.N;
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm) {
+      const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
+        if (m < p.M && n < p.N) *reinterpret_cast<f32x4*>(part + m * p.N + n) = acc[tm][tn];
+      }
+    }
+    return;
+  }
+  tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, 0, nk_all, smem, wave, lane, acc);
 
   if constexpr (BN == 256) {
     if (p.epi_lds) {
@@ -1311,6 +1328,28 @@ int launch8p(GemmArgs p, hipStream_t s) {
 // features) are cut into K chunks of >= 4 K-tiles, enough of them for ~512 workgroups.
 int g_splitk_blocks = 512;  // target blocks of a split-K launch (cullavo_gemm_set_splitk_target)
 
+// Split-K plan for the 8-wave 256x256 kernel: products whose 256x256 grid fills at most a
+// quarter of the CUs while K is long (the ViT's fc2 at 4 images: 2308 x 1024 x 4096; the
+// projector's weight gradients at 8 images: K = 4608): the K-tiles are cut into equal chunks of
+// >= 8 so tiles x splits is about one round of the 256 CUs; f32 partials [splits][M][N] are
+// reduced in split order (deterministic) by splitk_reduce_k with the full epilogue. Measured
+// (tools/small_gemm_bench.py, profiles/r03/small_gemm.txt): at K = 1024 the partials' round trip
+// costs more than the idle CUs (2308 x 3072 x 1024: 223 split vs 514 TF/s unsplit), at K >= 4096
+// the split wins (4096 x 1024 x 4608 dW: 652 vs 492). Both M and N >= 256 (else the 256-wide
+// tile is mostly padding: the register-staged 128x128 split below takes those).
+int num_cus();
+
+int splitk256_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
+  const int64_t tiles = cdiv(M, 256) * cdiv(N, 256), nk = cdiv(K, BK);
+  if (M < 256 || N < 256 || tiles * 4 > num_cus() || nk < 32) return 1;
+  int64_t s = std::min<int64_t>(num_cus() / tiles, nk / 8);
+  if (s < 2) return 1;
+  const int64_t per = cdiv(nk, s);
+  s = cdiv(nk, per);
+  if (kt_per) *kt_per = (int)per;
+  return (int)s;
+}
+
 int splitk_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
   const int64_t tiles = cdiv(M, BM) * cdiv(N, BN), nk = cdiv(K, BK);
   if (tiles >= 384 || nk < 8) return 1;
@@ -1396,6 +1435,15 @@ int launch256(GemmArgs p, hipStream_t s) {
   p.tiles_m = (int)cdiv(p.M, BM2);
   p.tiles_n = (int)cdiv(p.N, BN2);
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nk = cdiv(p.K, BK);
+  if (p.part) {  // split-K over the 8-wave kernel (small grids, splitk256_plan), then the reduce
+    const int splits = (int)cdiv(nk, p.kt_per);
+    p.sk_dp = (int)tiles;
+    p.sk_units = 0;
+    gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
+    const int64_t work = p.M * (p.N / 4);
+    splitk_reduce_k<CT><<<(int)std::min<int64_t>(cdiv(work, 256), 4096), 256, 0, s>>>(p, splits);
+    return cullavo_check_launch("gemm256 split-K");
+  }
   const int slots = num_cus();
   const int64_t full = tiles / slots, rem = tiles % slots;
   p.sk_dp = (int)tiles;
@@ -1521,6 +1569,14 @@ extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
 }
 
 extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid) {
+  if (g_force_tile < 0) {  // 9: the 8-wave 256x256 kernel split over K (given its workspace)
+    int per = 0;
+    const int s = splitk256_plan(M, N, K, &per);
+    if (s > 1) {
+      if (grid) *grid = cdiv(M, 256) * cdiv(N, 256) * s;
+      return 9;
+    }
+  }
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
   if (tile == 7 && a_layout != 0) tile = 6;
@@ -1590,23 +1646,26 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
                 (d.addend == nullptr || d.ld_addend % 8 == 0) && g_epi_lds;
   }
   p.nt_store = g_nt_store;
-  {
-    int per = 0;
-    const int splits = splitk_plan(M, N, K, &per);
-    const int64_t need = (int64_t)splits * M * N * 4;
-    if (splits > 1 && d.workspace != nullptr && d.workspace_bytes >= need && g_force_tile < 0) {
-      p.part = (float*)d.workspace;
-      p.kt_per = per;
-    }
-  }
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
   const int64_t b_ext = b_layout == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N;
   const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
+  bool split256 = false;
+  {
+    int per = 0, per256 = 0;
+    const int s256 = (dma_ok && d.drop_operand != 1 && d.drop_operand != 2) ? splitk256_plan(M, N, K, &per256) : 1;
+    const int splits = s256 > 1 ? s256 : splitk_plan(M, N, K, &per);
+    const int64_t need = (int64_t)splits * M * N * 4;
+    if (splits > 1 && d.workspace != nullptr && d.workspace_bytes >= need && g_force_tile < 0) {
+      p.part = (float*)d.workspace;
+      p.kt_per = s256 > 1 ? per256 : per;
+      split256 = s256 > 1;
+    }
+  }
   int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
   if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
-  if (p.part) tile = kT128;
+  if (p.part) tile = split256 ? kT256x256 : kT128;
   if (p.drop_mode == 1) return f32 ? launch<0, 0, CULLAVO_DT_F32, 1>(p, s) : launch<0, 0, CULLAVO_DT_BF16, 1>(p, s);
   if (p.drop_mode == 2) {
     if (a_layout == 0) return f32 ? launch<0, 1, CULLAVO_DT_F32, 2>(p, s) : launch<0, 1, CULLAVO_DT_BF16, 2>(p, s);
@@ -1669,7 +1728,9 @@ extern "C" size_t cullavo_gemm_desc_size(void) { return sizeof(cullavo_gemm_desc
 
 extern "C" size_t cullavo_gemm_workspace(const cullavo_gemm_desc* d) {
   if (d == nullptr || d->M <= 0 || d->N <= 0 || d->K <= 0 || g_force_tile >= 0) return 0;
-  const int splits = splitk_plan(d->M, d->N, d->K, nullptr);
+  const bool dma_layouts = d->drop_operand != 1 && d->drop_operand != 2;
+  const int s256 = dma_layouts ? splitk256_plan(d->M, d->N, d->K, nullptr) : 1;
+  const int splits = s256 > 1 ? s256 : splitk_plan(d->M, d->N, d->K, nullptr);
   return splits > 1 ? (size_t)splits * (size_t)d->M * (size_t)d->N * 4 : 0;
 }
 

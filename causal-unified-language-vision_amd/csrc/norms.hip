@@ -502,6 +502,7 @@ int nch_for(int64_t cols) {
   if (cols <= 1024) return 2;
   if (cols <= 2048) return 4;
   if (cols <= 4096) return 8;
+  if (cols <= 6144) return 12;  // Llama-2-13B's 5120: three chunks per wave in the 4-waves-per-row kernel
   return 16;
 }
 
@@ -511,6 +512,7 @@ int nch_for(int64_t cols) {
     case 2: { constexpr int NC = 2; __VA_ARGS__; break; } \
     case 4: { constexpr int NC = 4; __VA_ARGS__; break; } \
     case 8: { constexpr int NC = 8; __VA_ARGS__; break; } \
+    case 12: { constexpr int NC = 12; __VA_ARGS__; break; } \
     default: { constexpr int NC = 16; __VA_ARGS__; break; } \
   }
 
@@ -562,16 +564,19 @@ extern "C" int cullavo_rmsnorm_bwd(const void* dy, const void* x, const void* w,
   hipStream_t s = CV_STREAM(stream);
   const int nch = nch_for(cols);
   const bool want = dw != nullptr, hr = dres != nullptr;
-  const bool wide = nch > 8;  // 8192 columns: the 4-wave kernel (register budget)
-  // the pipelined kernel only pays when dw is wanted (measured, tools/norm_bench.py: without dw the
-  // round-1 kernel's four waves per SIMD already stream at ~5.8 TB/s)
-  const bool pipe = !wide && want && g_rms_bwd_mode == 1;
+  // more than 4096 columns (Llama-2-13B's 5120): the pipelined kernel with four waves per row
+  // (at most 4 x 8 bf16 per lane per tensor and register set); the round-1 one-wave-per-row kernel
+  // held 16 chunks of three tensors per lane and streamed 6400 x 5120 at 1.75 TB/s (config 5)
+  const bool wide = nch > 8 && g_rms_bwd_mode == 0;
+  // up to 4096 columns the pipelined kernel only pays when dw is wanted (measured,
+  // tools/norm_bench.py: without dw the round-1 kernel's four waves per SIMD stream at ~5.8 TB/s)
+  const bool pipe = !wide && g_rms_bwd_mode == 1 && (want || nch > 8);
   const int nb = wide ? bwd_blocks(rows) : (int)std::min<int64_t>(pipe ? kBwd8pBlocks : kBwd8Blocks, cdiv(rows, 4));
   const int64_t rpb = cdiv(rows, nb);
   const size_t lds = want ? (size_t)cols * sizeof(float) : 0;
 #define RMB(T, WD, HR)                                                                                        \
   if (wide) rmsnorm_bwd_k<T, 16, WD, HR><<<nb, 256, 0, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols); \
-  else if (pipe) NCH_DISPATCH(nch, rmsnorm_bwd8p_k<T, (NC > 8 ? 8 : NC), WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb)) \
+  else if (pipe) NCH_DISPATCH(nch, rmsnorm_bwd8p_k<T, NC, WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb)) \
   else NCH_DISPATCH(nch, rmsnorm_bwd8_k<T, (NC > 8 ? 8 : NC), WD, HR><<<nb, 512, lds, s>>>((const T*)dy, (const T*)x, (const T*)w, rstd, (T*)dx, (const T*)dres, ws, rows, (int)cols, rpb))
   if (dtype == CULLAVO_DT_BF16) {
     if (want && hr) { RMB(u16, true, true); } else if (want) { RMB(u16, true, false); }

@@ -69,6 +69,7 @@ class GradReducer:
         dev = arenas[0].flat.device if arenas else torch.device("cpu")
         self.stream = torch.cuda.Stream(device=dev) if (use_side_stream and dev.type == "cuda") else None
         self.enabled = self.world > 1 if enabled is None else (bool(enabled) and dist.is_initialized())
+        self.timing = None  # a list: record when each bucket becomes ready (overlap analysis)
         # host group for the written-key mask: the process group itself when it is gloo, else a
         # gloo group over the same ranks (created collectively here, as every rank builds its
         # reducer at the same point of init)
@@ -121,8 +122,10 @@ class GradReducer:
         view = ar.grad_flat[b["lo"]:b["hi"]]
         from .functions import dw_join, dw_wait
         if self.stream is not None:
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=self.timing is not None)
             ev.record(torch.cuda.current_stream(view.device))
+            if self.timing is not None:  # (bucket, bytes, ready event) for tools/dp_overlap.py
+                self.timing.append((bi, view.numel() * view.element_size(), ev))
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
                 dw_wait(self.stream)  # weight gradients of the bucket may be on the dW side stream

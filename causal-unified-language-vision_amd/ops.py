@@ -92,6 +92,19 @@ def trace_launches():
     return [(k, a.elapsed_time(b)) for a, b, k in evs]
 
 
+_SPLIT256 = {}
+
+
+def _split256(M, N, K, a_layout, b_layout) -> bool:
+    """the library runs this problem split over K on the 8-wave kernel (cullavo_gemm_plan tile 9:
+    a small 256x256 grid with a long K), given a workspace from the caller"""
+    key = (M, N, K, a_layout, b_layout)
+    v = _SPLIT256.get(key)
+    if v is None:
+        v = _SPLIT256[key] = lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None) == 9
+    return v
+
+
 def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
          alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
          beta: float = 0.0):
@@ -99,6 +112,9 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
     if A.dtype == torch.float32:  # f32 parity mode: every operand f32 (cullavo_gemm_ex f32_operands)
         return gemm_ex(a_layout, b_layout, M, N, K, A, lda, B, ldb, C, ldc, alpha=alpha, bias=bias, act=act,
                        preact=preact, residual=residual, ldr=ldr, beta=beta, split_k=False)
+    if _split256(M, N, K, a_layout, b_layout):  # small grid, long K: split-K with a torch workspace
+        return gemm_ex(a_layout, b_layout, M, N, K, A, lda, B, ldb, C, ldc, alpha=alpha, bias=bias, act=act,
+                       preact=preact, residual=residual, ldr=ldr, beta=beta)
     traced = _traced((M, N, K, a_layout, b_layout))
     if traced:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -149,7 +165,9 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
         if nbytes:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=C.device)
             d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
-    traced = not f32 and ws is None and not (drop_operand and drop_p > 0) and _traced((M, N, K, a_layout, b_layout))
+    # traced: the unsplit launches and the 8-wave split-K (bench.py names its family by cullavo_gemm_plan)
+    traced = (not f32 and (ws is None or _split256(M, N, K, a_layout, b_layout)) and not (drop_operand and drop_p > 0)
+              and _traced((M, N, K, a_layout, b_layout)))
     if traced:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(torch.cuda.current_stream())

@@ -152,7 +152,11 @@ int cullavo_gemm_set_splitk_target(int blocks);
    Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
- * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls. */
+ * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
+ * 9 = the 8-wave 256x256 kernel split over K (a grid of fewer than half the CUs with >= 8
+ * K-tiles, both M and N >= 256): used by cullavo_gemm_ex when the caller passes the workspace
+ * cullavo_gemm_workspace() asks for; f32 partials [splits][M][N], reduced in split order
+ * (deterministic) with the full epilogue. cullavo_gemm itself (no workspace) never splits. */
 int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid);
 
 /* ---- norms -------------------------------------------------------------------------------

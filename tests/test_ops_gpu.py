@@ -263,7 +263,7 @@ def test_gemm_pipelined_repeatable(al, bl):
 # ---------------------------------------------------------------------------------------------
 # norms
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("rows,cols", [(64, 4096), (37, 1024), (5, 128), (9, 8192)])
+@pytest.mark.parametrize("rows,cols", [(64, 4096), (37, 1024), (5, 128), (9, 8192), (97, 5120)])
 def test_rmsnorm(rows, cols):
     x, w = rnd((rows, cols), 20), (1 + 0.1 * rnd((cols,), 21).float()).to(BF)
     y, rstd = ops().rmsnorm_fwd(x.to(DEV), w.to(DEV), 1e-5)
@@ -280,10 +280,12 @@ def test_rmsnorm(rows, cols):
     close(dw, wr.grad, 1e-2, "rms dw")
 
 
-@pytest.mark.parametrize("rows,cols", [(8704, 4096), (1037, 4096), (3, 4096), (515, 1024)])
+@pytest.mark.parametrize("rows,cols", [(8704, 4096), (1037, 4096), (3, 4096), (515, 1024), (6400, 5120),
+                                       (131, 8192)])
 def test_rmsnorm_bwd_modes(rows, cols):
-    """Pipelined backward (mode 1, default) vs the round-1 kernel (mode 0) and the oracle, at the
-    config-3 shape and ragged row counts (partial last iterations / empty workgroups)."""
+    """Pipelined backward (mode 1, default) vs the round-1 kernels (mode 0) and the oracle, at the
+    config-3 and config-5 (d 5120) shapes and ragged row counts (partial last iterations / empty
+    workgroups); with and without the weight gradient."""
     from cullavo_amd import _lib
     x, w = rnd((rows, cols), 40), (1 + 0.1 * rnd((cols,), 41).float()).to(BF)
     dy, dres = rnd((rows, cols), 42), rnd((rows, cols), 43)
@@ -298,11 +300,18 @@ def test_rmsnorm_bwd_modes(rows, cols):
             dx2 = ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV), dw=dw)
             assert torch.equal(dx, dx2), "rmsnorm_bwd is not deterministic"
             outs[mode] = (dx.float(), dw.clone())
+        for mode in (0, 1):  # no weight gradient (frozen norms: the LoRA recipe)
+            L.cullavo_rmsnorm_set_bwd(mode)
+            dxn = ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV))
+            assert torch.equal(dxn, ops().rmsnorm_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), rstd, dres=dres.to(DEV)))
+            outs[("nodw", mode)] = dxn.float()
     finally:
         L.cullavo_rmsnorm_set_bwd(1)
     (dx0, dw0), (dx1, dw1) = outs[0], outs[1]
     # same per-element arithmetic; only the row dot product's partial-sum order differs
     assert (dx1 - dx0).abs().max().item() <= 2 * (dx0.abs().max().item() * 2 ** -7)
+    assert (outs[("nodw", 1)] - dx0).abs().max().item() <= 2 * (dx0.abs().max().item() * 2 ** -7)
+    assert (outs[("nodw", 0)] - dx0).abs().max().item() <= 2 * (dx0.abs().max().item() * 2 ** -7)
     assert ((dw1 - dw0).norm() / dw0.norm()).item() < 1e-5
     xr = x.float().requires_grad_(True)
     wr = w.float().requires_grad_(True)
@@ -369,6 +378,52 @@ def test_swiglu_bwd_fused_in_dx_gemm(M, Fd, d, tile):
     assert torch.equal(fused_t, ref)
     with pytest.raises(Exception):
         ops().linear_dx(dy, w, swiglu_gu=gu[:, :Fd])
+
+
+@pytest.mark.parametrize("M,N,K,al,bl,epi", [(2308, 1024, 4096, 0, 0, "bias_res"), (1024, 1024, 8192, 0, 0, "quick_gelu"),
+                                              (4096, 1024, 4608, 1, 1, "beta"), (2304, 1024, 5120, 0, 1, "none"),
+                                              (1032, 520, 8192, 0, 0, "bias")])
+def test_gemm_split256_small_grid(M, N, K, al, bl, epi):
+    """Small 256x256 grids with a long K (the ViT's fc2 at 4 images, the projector's weight
+    gradient at 8 images, ragged edges) run split over K on the 8-wave kernel (cullavo_gemm_plan tile 9) with a torch
+    workspace: fp32-product parity with every epilogue it carries, deterministic (bitwise equal
+    across launches) and within a bf16 ulp of the unsplit kernel (forced tile 2)."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    assert L.cullavo_gemm_plan(M, N, K, al, bl, None) == 9
+    A = rnd((K, M) if al else (M, K), 80).to(DEV)
+    B = rnd((K, N) if bl else (N, K), 81).to(DEV)
+    bias = rnd((N,), 82).to(DEV) if epi in ("bias", "bias_res", "quick_gelu") else None
+    res = rnd((M, N), 83).to(DEV) if epi == "bias_res" else None
+    act = ops().ACT_QUICK_GELU if epi == "quick_gelu" else ops().ACT_NONE
+    beta = 1.0 if epi == "beta" else 0.0
+    C0 = rnd((M, N), 84).to(DEV)
+
+    def run():
+        C = C0.clone()
+        ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, act=act, residual=res,
+                   ldr=N if res is not None else 0, beta=beta)
+        return C
+    c1, c2 = run(), run()
+    assert torch.equal(c1, c2)
+    prev = L.cullavo_gemm_set_tile(2)
+    try:
+        c_ref = run()
+    finally:
+        L.cullavo_gemm_set_tile(prev)
+    Am = (A.float().T if al else A.float())
+    Bm = (B.float() if bl else B.float().T)
+    z = Am @ Bm
+    if bias is not None:
+        z = z + bias.float()
+    if act == ops().ACT_QUICK_GELU:
+        z = O.quick_gelu(z.to(BF).float())
+    if res is not None:
+        z = z.to(BF).float() + res.float()
+    z = z + beta * C0.float()
+    close(c1, z, 8e-3, f"split-K {M}x{N}x{K}")
+    diff = (c1.float() - c_ref.float()).abs()
+    assert diff.max().item() <= 2 ** -6 * c_ref.float().abs().max().item(), diff.max().item()
 
 
 @pytest.mark.parametrize("act", [1, 2])
