@@ -93,6 +93,7 @@ DEV frag8 pack_frag(const f32x16& a, int s) {
 // its byte offsets fit 32 bits unless nrows * ld is very large; then the pointer path runs.
 constexpr unsigned kOOB = 0x7FFFFFF0u;
 
+__device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (cullavo_attn_set_rescale)
 __device__ int g_stage_buf = 1;  // A/B switch (cullavo_attn_set_stage): 0 = pointer loads everywhere
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return g_stage_buf && ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   for (int i = 0; i < ND; ++i) o[i] = f32x16(0.f);
   float m = -INFINITY, l = 0.f;
   const float c = scale * kLog2e;
+  const float rescale_thr = g_rescale_thr;
 
   // live keys of this lane's query: [kstart, khi)
   const int khi = CAUSAL ? min(Lk, q + 1) : Lk;
@@ -268,9 +270,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, st[kt][r]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c;
-    const float mnew = fmaxf(m, tmax);
-    const float muse = (mnew == -INFINITY) ? 0.f : mnew;
-    const float alpha = fast_exp2(m - muse);
+    // Deferred rescale (cdna_hip_programming.md T13): the reference max m moves -- and O, l are
+    // rescaled by exp2(m_old - m_new) -- only on tiles where some row's max grew by more than
+    // g_rescale_thr (log2 units); otherwise P = exp2(s c - m) <= 2^thr against the stale m (f32,
+    // and bf16 keeps its relative precision at that scale) and the 64 O multiplies per tile are
+    // skipped. LSE = m + log2(l) is exact either way. thr = 0 rescales whenever a max grows:
+    // bitwise the plain online softmax (a tile that grows no max has alpha = 1 on every lane).
+    float muse;
+    if (__any(tmax > m + rescale_thr)) {  // wave-uniform
+      const float mnew = fmaxf(m, tmax);
+      muse = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = fast_exp2(m - muse);
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) o[i] *= alpha;
+      m = mnew;
+    } else {
+      muse = (m == -INFINITY) ? 0.f : m;
+    }
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -281,10 +298,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
         rs += pv;
       }
     rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mnew;
-#pragma unroll
-    for (int i = 0; i < ND; ++i) o[i] *= alpha;
+    l += rs;
     // O^T += V^T P^T
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -1375,6 +1389,14 @@ extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int v = buffer_loads ? 1 : 0;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage_buf), &v, sizeof(int)) != hipSuccess) return -1;
   return prev;
+}
+
+extern "C" int cullavo_attn_set_rescale(float threshold, float* previous) {
+  CV_REQUIRE(threshold >= 0.f && threshold <= 16.f, CULLAVO_EINVAL, "rescale threshold must be in [0, 16]");
+  if (previous && hipMemcpyFromSymbol(previous, HIP_SYMBOL(g_rescale_thr), sizeof(float)) != hipSuccess)
+    return CULLAVO_EHIP;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_rescale_thr), &threshold, sizeof(float)) != hipSuccess) return CULLAVO_EHIP;
+  return CULLAVO_OK;
 }
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {

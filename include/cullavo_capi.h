@@ -260,6 +260,12 @@ int cullavo_attn_set_bwd_tiles(int mode);
    bounds branch. Results are identical. Synchronous (device symbol copy); returns the previous
    setting, -1 on a HIP error. */
 int cullavo_attn_set_stage(int buffer_loads);
+/* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
+   move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in
+   [0, 16]; default 8: softmax weights stay <= 2^8 against the stale max, LSE exact). 0 = rescale
+   whenever a max grows, bitwise the plain online softmax. Synchronous (device symbol copy);
+   *previous (nullable) receives the old threshold. */
+int cullavo_attn_set_rescale(float threshold, float* previous);
 
 /* ---- KV-cache decode (generate) --------------------------------------
  * Cache per layer: K, V [B, Lmax, H*D] bf16, token stride ld_tok, batch stride ld_batch.

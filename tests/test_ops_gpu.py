@@ -7,6 +7,8 @@ index work (merge plan, targets, gathers, embedding rows) bit-exactly.
 """
 import math
 
+import ctypes
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -510,6 +512,48 @@ def test_attention_fwd_bwd(B, H, L, D, causal):
     close(dv, tr(vf.grad), 2e-2, "dv")
     close(dk, tr(kf.grad), 2e-2, "dk")
     close(dq, tr(qf.grad), 2e-2, "dq")
+
+
+@pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
+def test_attention_fwd_deferred_rescale_forced(D, causal):
+    """The forward's deferred rescale (cullavo_attn_set_rescale, guide T13 / rule 26): inputs that
+    FORCE the rare branch -- a spike key late in the sequence whose score jumps far above every
+    earlier one for most queries, so the running max must move by more than the threshold at a
+    late tile -- checked against a float64 reference at thresholds 0 (rescale on every growth,
+    the plain online softmax), 8 (default) and 16, with LSE agreeing to 1e-5 across them."""
+    from cullavo_amd import _lib
+    B, H, L = 2, 2, 300
+    u = rnd((1, 1, H, D), 78).float()                     # a direction every query shares
+    q = (rnd((B, L, H, D), 75).float() + u).reshape(B * L, H * D).to(BF)
+    kh = rnd((B, L, H, D), 76).float()
+    v = rnd((B * L, H * D), 77)
+    spike = 230  # a key in the 4th 64-key tile scoring ~3D / sqrt(D) against every query
+    kh[:, spike] = 3.0 * u[0, 0]
+    k = kh.reshape(B * L, H * D).to(BF)
+    kw = dict(B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal)
+    L_ = _lib.lib()
+    outs = {}
+    prev = ctypes.c_float(0.0)
+    try:
+        for thr in (0.0, 8.0, 16.0):
+            assert L_.cullavo_attn_set_rescale(ctypes.c_float(thr), ctypes.addressof(prev)) == 0
+            outs[thr] = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
+    finally:
+        L_.cullavo_attn_set_rescale(ctypes.c_float(8.0), None)
+    qd = q.double().view(B, L, H, D).transpose(1, 2)
+    kd = k.double().view(B, L, H, D).transpose(1, 2)
+    vd = v.double().view(B, L, H, D).transpose(1, 2)
+    sc = (qd @ kd.transpose(-1, -2)) * D ** -0.5
+    if causal:
+        sc = sc.masked_fill(~torch.ones(L, L, dtype=torch.bool).tril(), float("-inf"))
+    assert (sc[..., spike:, spike] - sc[..., spike:, :spike].amax(-1)).median() * 1.4427 > 16  # branch forced
+    o_ref = (torch.softmax(sc, -1) @ vd).transpose(1, 2).reshape(B * L, H * D)
+    for thr, (o, lse) in outs.items():
+        close(o, o_ref, 1.2e-2, f"attn o, threshold {thr}")
+        close(lse, torch.logsumexp(sc, -1), 1e-4, f"lse, threshold {thr}")
+        assert ((lse - outs[0.0][1]).abs() / outs[0.0][1].abs().clamp_min(1.0)).max().item() < 1e-5
+    with pytest.raises(ValueError):
+        _lib.call("attn_set_rescale", ctypes.c_float(-1.0), None)
 
 
 @pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
