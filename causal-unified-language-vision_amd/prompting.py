@@ -313,13 +313,15 @@ def box_and_class_parser(decoded_text: str):
     return torch.tensor(boxes), classes, False
 
 
-def step2_preprocess(model, batched_inputs, processor, device, *, dice=None, generate_kwargs=None, on_generate=None):
+def step2_preprocess(model, batched_inputs, processor, device, *, dice=None, generate_kwargs=None, on_generate=None,
+                     vis_dir=None):
     """reference cullavo/arch_cullavo.py:341-395: for one record in ~50 (torch.randint(0, 50) == 0)
     generate an object/box description of its image with the reference's sampling settings
     (T 0.9, top-k 50, top-p 0.95, 1000 new tokens, KV cache), parse boxes and classes, and emit
-    the new lbk.json entry; every other record passes through. The reference also rasterises the
-    boxes into the image with detectron2's Visualizer and saves it (:376-386): that drawing is
-    out of scope here, the entry carries the parsed boxes/classes for it. dice(record) replaces
+    the new lbk.json entry; every other record passes through. With vis_dir the image with the
+    boxes (x 336) and class names is written to vis_dir/<question_id>.png like the reference's
+    debugging render (:376-386, visualize.render_boxes_and_labels); a failing render emits the
+    record without boxes, as the reference's bare except does. dice(record) replaces
     the random roll, generate_kwargs override the sampling settings (tests: greedy),
     on_generate(record, generate_ids, decoded_text) observes each generation."""
     gk = dict(STEP2_PRE_GENERATE, **(generate_kwargs or {}))
@@ -350,6 +352,16 @@ def step2_preprocess(model, batched_inputs, processor, device, *, dice=None, gen
                 # (utils/visualizer.py:673) and the bare except emits the record without boxes
                 new.append(base)
                 continue
+            if vis_dir is not None:
+                import os
+
+                from PIL import Image
+
+                from .visualize import render_boxes_and_labels
+                n = boxes.shape[0]
+                img = render_boxes_and_labels(batch["image"], boxes[:len(COLOR_LIST)] * 336, classes,
+                                              COLOR_LIST[:n])
+                Image.fromarray(img).save(os.path.join(vis_dir, f"{batch['question_id']}.png"))
             new.append(dict(base, boxes=boxes.cpu().tolist(), classes=classes))
         except Exception:  # the reference's bare except (:387-388)
             new.append(base)

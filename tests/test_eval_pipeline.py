@@ -87,6 +87,32 @@ def test_step2_preprocess_more_boxes_than_colors(monkeypatch, n_boxes):
         assert out[0]["classes"] == [f"#{i}" for i in range(n_boxes)] and len(out[0]["boxes"]) == n_boxes
 
 
+def test_step2_preprocess_visualisation_png(monkeypatch, tmp_path):
+    """vis_dir: the record's image with its generated boxes (x 336) and class names is written to
+    <vis_dir>/<question_id>.png (reference cullavo/arch_cullavo.py:376-386): right size, the
+    box edges drawn in their colours, the labels on black boxes; the entry carries the boxes."""
+    import numpy as np
+    from PIL import Image
+    from cullavo_amd import prompting as P
+    text = "Sure. cat (#1) [0.100, 0.100, 0.600, 0.700], dog (#2) [0.500, 0.550, 0.950, 0.950]"
+    monkeypatch.setattr(P, "eval_process", lambda **kw: {})
+    model = SimpleNamespace(config=SimpleNamespace(ignore_index=-100), generate=lambda **kw: torch.zeros(1, 3))
+    proc = SimpleNamespace(batch_decode=lambda ids, skip_special_tokens=True: [text])
+    img = torch.full((3, 336, 336), 128, dtype=torch.uint8)
+    rec = {"question_id": "q7", "image_id": "a.jpg", "image": img, "question": [{"from": "human", "value": "<image>"}]}
+    out = P.step2_preprocess(model, [rec], proc, "cpu", dice=lambda r: 0, vis_dir=str(tmp_path))
+    assert out[0]["classes"] == ["#1", "#2"] and len(out[0]["boxes"]) == 2
+    png = np.asarray(Image.open(tmp_path / "q7.png").convert("RGB"))
+    assert png.shape == (336, 336, 3)
+    assert (png != 128).any(axis=2).mean() > 0.01          # boxes and labels were drawn
+    assert (png[200, 33:36] != 128).any()                   # cat's left edge (x = 33.6) in white/red
+    assert (png[:, :, :] < 60).all(axis=2).any()            # the labels' black boxes
+    # a render that fails (here: an unreadable image) falls back to the record without boxes
+    bad = dict(rec, question_id="q8", image=object())
+    out = P.step2_preprocess(model, [bad], proc, "cpu", dice=lambda r: 0, vis_dir=str(tmp_path))
+    assert out == [{"id": "q8", "image": "a.jpg", "conversations": rec["question"]}]
+
+
 def _processor(size):
     from cullavo_amd.prompting import ClipImageProcessorHIP, CuLLaVOProcessor
     return CuLLaVOProcessor(TinyVocabTokenizer(), ClipImageProcessorHIP(shortest_edge=size, crop_size=size))
