@@ -99,6 +99,10 @@ def lib():
             L.cullavo_gemm_set_splitk_target(int(os.environ["CULLAVO_SPLITK_TARGET"]))
         if os.environ.get("CULLAVO_GEMM_GROUP"):  # tile-order A/B (cullavo_gemm_set_group)
             L.cullavo_gemm_set_group(int(os.environ["CULLAVO_GEMM_GROUP"]))
+        if os.environ.get("CULLAVO_GEMM_DMA"):  # DMA-offset A/B (cullavo_gemm_set_dma)
+            L.cullavo_gemm_set_dma(int(os.environ["CULLAVO_GEMM_DMA"]))
+        if os.environ.get("CULLAVO_ATTN_RESCALE"):  # deferred-rescale A/B (cullavo_attn_set_rescale)
+            L.cullavo_attn_set_rescale(float(os.environ["CULLAVO_ATTN_RESCALE"]), None)
     return _lib
 
 

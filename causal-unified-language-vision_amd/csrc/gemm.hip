@@ -54,6 +54,7 @@ struct GemmArgs {
   float* sk_ws;       // f32 partials [sk_units][2][512 threads x TMW*TN f32x4], fragment order
   int group_m;        // 8-wave tile order: > 0 groups of group_m M-tiles sweep N; < 0 groups of
                       // -group_m N-tiles sweep M
+  int dma_pre;        // 8-wave 256-row kernels: per-lane DMA offsets precomputed, K advance in soffset
 };
 
 template <typename V>
@@ -566,6 +567,49 @@ DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t
   }
 }
 
+// Same pieces with the per-lane source offsets computed once per tile (dma_prep) and the K
+// advance passed as the instruction's scalar offset (dma_issue): a K-tile's issue is then one
+// m0 write + one buffer_load per piece instead of 64-bit address math and exec-masked range
+// selects per piece. Out-of-range rows get kOOBp, which stays past num_records with any K
+// advance added. Layout 1 needs no K-range check (rows k >= K lie past the buffer's extent,
+// (K-1)*ld + idx_max, as ld >= idx_max); layout 0 needs full K-tiles (gk < K), so the caller
+// uses it only when K % 64 == 0 for every layout-0 operand.
+constexpr unsigned kOOBp = 0x80000000u;
+
+template <int LAYOUT, int ROWS, int NW>
+DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane, unsigned (&vo)[ROWS / 8 / NW]) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 8 / NW; ++i) {
+    const int pc = wave + NW * i;
+    int64_t gi, rel;
+    if (LAYOUT == 0) {
+      const int row = pc * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      gi = idx0 + row;
+      rel = gi * ld + chunk * 8;
+    } else {
+      constexpr int RB = ROWS * 2;
+      const int byte = pc * 1024 + lane * 16;
+      const int k = byte / RB, b = byte % RB;
+      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+      gi = idx0 + unit * 16 + half * 8;
+      rel = k * ld + gi;
+    }
+    vo[i] = gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
+  }
+}
+
+template <int ROWS, int NW>
+DEV void dma_issue(__amdgpu_buffer_rsrc_t rsrc, const unsigned* vo, int soff, char* lds, int wave) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 8 / NW; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (wave + NW * i) * 1024), 16, vo[i], soff, 0, 0);
+}
+
+// scalar byte offset of K-tile origin k0 for an operand of layout L
+template <int L>
+DEV int dma_soff(int64_t k0, int64_t ld) { return (int)(L == 0 ? k0 * 2 : k0 * ld * 2); }
+
 template <int ROWS>
 DEV int img1w_off(int k, int unit) { return k * (ROWS * 2) + ((unit ^ swz1(k)) << 5); }
 
@@ -631,6 +675,40 @@ DEV frag8 read_frag_w(const char* lds, int rbase, int ks, int lane) {
   return __builtin_bit_cast(frag8, v);
 }
 
+// one K-tile of MFMAs from the LDS stage at cur (both 32-wide K halves)
+template <int AL, int BL, int BM2, int BN, int TMW, int TN>
+DEV void tile_mfma(const char* cur_c, int wm, int wn, int lane, f32x4 (&acc)[TMW][TN]) {
+  constexpr int TILE_A = BM2 * BK * 2;
+  constexpr int WN_COLS = BN / 4;
+  char* cur = const_cast<char*>(cur_c);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    frag8 fb[TN];
+    s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
+    if constexpr (BL == 1) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) tr_issue<BN>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane, blo[t], bhi[t]);
+    }
+    if constexpr (AL == 1) {
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * (BM2 / 2) + tm * 16, ks, lane, alo[tm], ahi[tm]);
+    }
+    if constexpr (BL == 1) tie_all<TN>(blo, bhi);
+    if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
+    if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+      fb[t] = BL == 1 ? tr_join(blo[t], bhi[t]) : read_frag<0>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane);
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm) {
+      const frag8 fa = AL == 1 ? tr_join(alo[tm], ahi[tm]) : read_frag<0>(cur, wm * (BM2 / 2) + tm * 16, ks, lane);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
+    }
+  }
+}
+
 // LDR selects which waves stage the next K-tile: 0 = all eight (each wave issues its share of
 // LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
 // 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
@@ -643,7 +721,6 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
   constexpr int TILE_A = BM2 * BK * 2;
   constexpr int TILE_B = BN * BK * 2;
   constexpr int STAGE = TILE_A + TILE_B;
-  constexpr int WN_COLS = BN / 4;
   const int wm = wave >> 2, wn = wave & 3;
 #pragma unroll
   for (int i = 0; i < TMW; ++i)
@@ -654,6 +731,28 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
   dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, (int64_t)kb * BK, p.K, smem + TILE_A, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+
+  if (p.dma_pre) {
+    constexpr int NWL = LDR == 0 ? 8 : 4;
+    const int lw = LDR == 0 ? wave : (wave & 3);
+    const bool loader = LDR == 0 || (LDR == 1 ? wave < 4 : wave >= 4);
+    unsigned va[BM2 / 8 / NWL], vb[BN / 8 / NWL];
+    dma_prep<AL, BM2, NWL>(p.lda, m0, p.M, lw, lane, va);
+    dma_prep<BL, BN, NWL>(p.ldb, n0, p.N, lw, lane, vb);
+    for (int kt = kb; kt < ke; ++kt) {
+      char* cur = smem + ((kt - kb) & 1) * STAGE;
+      char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
+      const int64_t k1 = (int64_t)(kt + 1) * BK;
+      if (kt + 1 < ke && loader) {
+        dma_issue<BM2, NWL>(ra, va, dma_soff<AL>(k1, p.lda), nxt, lw);
+        dma_issue<BN, NWL>(rb, vb, dma_soff<BL>(k1, p.ldb), nxt + TILE_A, lw);
+      }
+      tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    return;
+  }
 
   for (int kt = kb; kt < ke; ++kt) {
     char* cur = smem + ((kt - kb) & 1) * STAGE;
@@ -675,32 +774,7 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
         }
       }
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      frag8 fb[TN];
-      s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
-      if constexpr (BL == 1) {
-#pragma unroll
-        for (int t = 0; t < TN; ++t) tr_issue<BN>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane, blo[t], bhi[t]);
-      }
-      if constexpr (AL == 1) {
-#pragma unroll
-        for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * (BM2 / 2) + tm * 16, ks, lane, alo[tm], ahi[tm]);
-      }
-      if constexpr (BL == 1) tie_all<TN>(blo, bhi);
-      if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
-      if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < TN; ++t)
-        fb[t] = BL == 1 ? tr_join(blo[t], bhi[t]) : read_frag<0>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane);
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm) {
-        const frag8 fa = AL == 1 ? tr_join(alo[tm], ahi[tm]) : read_frag<0>(cur, wm * (BM2 / 2) + tm * 16, ks, lane);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
-      }
-    }
+    tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -1532,6 +1606,7 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 static int g_force_tile = -1;
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
+static int g_dma_pre = 1;  // +2.7 % on the 7B step (profiles/r03/dma_ab.md)
 // Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
 // step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
 static int g_group_m = -4;
@@ -1557,6 +1632,13 @@ extern "C" int cullavo_gemm_set_streamk(int mode) {
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
   g_force_tile = (mode >= 0 && mode <= 8) ? mode : -1;
+  return prev;
+}
+
+// A/B switch for the precomputed-offset LDS-DMA loop of the 8-wave 256-row kernels
+extern "C" int cullavo_gemm_set_dma(int precomputed) {
+  const int prev = g_dma_pre;
+  g_dma_pre = precomputed & 1;
   return prev;
 }
 
@@ -1646,6 +1728,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
                 (d.addend == nullptr || d.ld_addend % 8 == 0) && g_epi_lds;
   }
   p.nt_store = g_nt_store;
+  p.dma_pre = g_dma_pre && (a_layout == 1 || K % BK == 0) && (b_layout == 1 || K % BK == 0);
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;

@@ -151,6 +151,11 @@ int cullavo_gemm_set_splitk_target(int blocks);
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
    Bit 1: C is written with non-temporal (streaming) stores. Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
+/* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets
+   computed once per tile and the K advance passed as the scalar offset (used when K % 64 == 0
+   or the operand is stored [K][rows], layout 1; the default); 0 = offsets recomputed per
+   K-tile. Same results either way. Returns the previous setting. */
+int cullavo_gemm_set_dma(int precomputed);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
  * 9 = the 8-wave 256x256 kernel split over K (a grid of fewer than half the CUs with >= 8

@@ -428,6 +428,42 @@ def test_gemm_split256_small_grid(M, N, K, al, bl, epi):
     assert diff.max().item() <= 2 ** -6 * c_ref.float().abs().max().item(), diff.max().item()
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7])
+@pytest.mark.parametrize("al,bl,K", [(0, 0, 1024), (0, 1, 576), (1, 0, 640), (1, 1, 1000), (1, 1, 4096), (0, 0, 1000)])
+def test_gemm_dma_precomputed_offsets_bitwise(tile, al, bl, K):
+    """The precomputed-offset LDS-DMA loop (cullavo_gemm_set_dma(1): per-lane source offsets once
+    per tile, K advance in the scalar offset) loads the same bytes as the per-K-tile path, so the
+    8-wave kernels' outputs are bitwise equal with it on or off: every layout pair, ragged M/N
+    edges (rows past M / N read as zeros), a K tail on layout-1 operands (rows past K lie past the
+    buffer), both loader choices (tiles 6/7 flip LDR), and the fallback when a layout-0 operand
+    has K % 64 != 0 (K 1000 with al = 0)."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    if tile in (3, 7) and al == 1:
+        pytest.skip("192-row tiles take a layout-0 A only")
+    M, N = 1000, 776
+    A = rnd((K, M) if al else (M, K), 90).to(DEV)
+    B = rnd((K, N) if bl else (N, K), 91).to(DEV)
+    bias = rnd((N,), 92).to(DEV)
+    outs = []
+    prev_t = L.cullavo_gemm_set_tile(tile)
+    try:
+        for mode in (0, 1, 0):
+            prev = L.cullavo_gemm_set_dma(mode)
+            C = torch.empty((M, N), dtype=BF, device=DEV)
+            ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias)
+            torch.cuda.synchronize()
+            L.cullavo_gemm_set_dma(prev)
+            outs.append(C)
+    finally:
+        L.cullavo_gemm_set_tile(prev_t)
+    assert torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()
+    Am = (A.float().T if al else A.float())
+    Bm = (B.float() if bl else B.float().T)
+    close(outs[1], Am @ Bm + bias.float(), 8e-3, f"dma_pre tile {tile} {al}{bl} K={K}")
+
+
 @pytest.mark.parametrize("act", [1, 2])
 def test_act_bwd(act):
     x = rnd((33, 256), 50, 2.0)

@@ -29,6 +29,8 @@ def main():
         kw = dict(B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal)
         fl = 4.0 * B * H * L * L * D * (0.5 if causal else 1.0)
         res = {0.0: [], 8.0: []}
+        for _ in range(200):  # clocks up to the sustained level before timing
+            ops.attn_fwd(q, k, v, **kw)
         for _ in range(a.rounds):
             for thr in res:
                 L_.cullavo_attn_set_rescale(ctypes.c_float(thr), None)

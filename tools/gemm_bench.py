@@ -60,7 +60,8 @@ def main():
                 lib.cullavo_gemm_set_group(grp)
                 lane_epi = "L" in mode  # e.g. "-1L": same kernel, per-lane epilogue
                 nt = "N" in mode        # e.g. "-1N": non-temporal C stores
-                lib.cullavo_gemm_set_tile(int(mode.rstrip("LN")))
+                lib.cullavo_gemm_set_dma(0 if "D" in mode else 1)  # "-1D": per-K-tile DMA offsets
+                lib.cullavo_gemm_set_tile(int(mode.rstrip("LND")))
                 lib.cullavo_gemm_set_epilogue((0 if lane_epi else 1) | (2 if nt else 0))
                 o = ours[kind]()
                 err = ((o.float() - r.float()).norm() / r.float().norm()).item()
@@ -68,6 +69,7 @@ def main():
                 line += f" | m{mode}g{grp} {fl / t / 1e9:7.1f} TF err {err:.1e}"
             lib.cullavo_gemm_set_tile(-1)
             lib.cullavo_gemm_set_epilogue(1)
+            lib.cullavo_gemm_set_dma(1)
             lib.cullavo_gemm_set_group(-4)
             print(line, flush=True)
 
