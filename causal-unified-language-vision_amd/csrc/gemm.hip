@@ -543,8 +543,9 @@ DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t
   if (LAYOUT == 0) {
     constexpr int kPieces = ROWS / 8;  // 8 rows of 128 B per 1 KiB piece
 #pragma unroll
-    for (int i = 0; i < kPieces / NW; ++i) {
+    for (int i = 0; i < (kPieces + NW - 1) / NW; ++i) {
       const int pc = wave + NW * i;
+      if (kPieces % NW != 0 && pc >= kPieces) break;  // 288 rows = 36 pieces over 8 waves (wave-uniform)
       const int row = pc * 8 + (lane >> 3);
       const int chunk = (lane & 7) ^ ((row >> 1) & 7);
       const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
@@ -578,6 +579,7 @@ constexpr unsigned kOOBp = 0x80000000u;
 
 template <int LAYOUT, int ROWS, int NW>
 DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane, unsigned (&vo)[ROWS / 8 / NW]) {
+  static_assert((ROWS / 8) % NW == 0, "LDS-DMA pieces must split evenly over the loader waves");
 #pragma unroll
   for (int i = 0; i < ROWS / 8 / NW; ++i) {
     const int pc = wave + NW * i;
@@ -1499,7 +1501,8 @@ float* sk_workspace(hipStream_t s) {
 
 template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0>
 int launch256(GemmArgs p, hipStream_t s) {
-  const int smem = 2 * (BM2 * BK * 2 + BN2 * BK * 2);
+  // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB)
+  const int smem = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR>,
@@ -1579,16 +1582,24 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
 // and the box-to-box spread (~10 %) is larger than their forward gain. With the steady DMA
 // removed the same schedule reaches hipBLASLt's rate (gate|up 1483 vs 1382 TF/s), so the
 // remaining loss is LDS-DMA issue cost inside the load segment (profiles/r01/gemm_8phase.md).
-enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8 };
+// kT288x256 (round 3): 288-row tiles for a K-contiguous A (9 MFMA rows per wave, 36 A pieces
+// over the 4 loader waves). The per-K-tile overhead (barrier, DMA issue, fragment-read latency)
+// is roughly fixed, so a taller tile amortises it over more MFMAs, and M = 8704 = 30.2 x 288
+// makes the N = 4096 products (every dX, o and down forward) 496 tiles = 1.94 rounds instead of
+// 736 192-row tiles = 2.88 rounds.
+enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8, kT288x256 = 10 };
+// plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
+double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
-  const C cands[3] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, 1300.0},
-                      {kT192x256, 192, 256, 256, 1150.0}};
+  const C cands[4] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, g_tile_rate[0]},
+                      {kT192x256, 192, 256, 256, g_tile_rate[1]}, {kT288x256, 288, 256, 256, g_tile_rate[2]}};
   double best = 1e300;
   int bid = kT128;
   for (const C& c : cands) {
-    if (c.id == kT192x256 && a_layout != 0) continue;
+    if ((c.id == kT192x256 || c.id == kT288x256) && a_layout != 0) continue;
+    if (c.rate <= 0.0) continue;
     const int64_t tiles = cdiv(M, c.bm) * cdiv(N, c.bn);
     const double exact = (double)tiles / (double)c.slots;
     const double rounds = (double)cdiv(tiles, c.slots);
@@ -1631,8 +1642,17 @@ extern "C" int cullavo_gemm_set_streamk(int mode) {
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = (mode >= 0 && mode <= 8) ? mode : -1;
+  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256) ? mode : -1;
   return prev;
+}
+
+extern "C" int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous) {
+  const int i = mode == kT256x256 ? 0 : mode == kT192x256 ? 1 : mode == kT288x256 ? 2 : -1;
+  CV_REQUIRE(i >= 0, CULLAVO_EINVAL, "tile rate: mode must be 2, 3 or 10");
+  CV_REQUIRE(i != 0 || tflops > 0.f, CULLAVO_EINVAL, "tile rate: mode 2 cannot be removed");
+  if (previous) *previous = (float)g_tile_rate[i];
+  g_tile_rate[i] = tflops > 0.f ? (double)tflops : 0.0;
+  return CULLAVO_OK;
 }
 
 // A/B switch for the precomputed-offset LDS-DMA loop of the 8-wave 256-row kernels
@@ -1660,10 +1680,10 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
     }
   }
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
-  if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
   if (tile == 7 && a_layout != 0) tile = 6;
-  static const int bm[9] = {128, 256, 256, 192, 256, 256, 256, 192, 256};
-  static const int bn[9] = {128, 128, 256, 256, 256, 256, 256, 256, 256};
+  static const int bm[11] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288};
+  static const int bn[11] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -1747,7 +1767,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     }
   }
   int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
-  if (tile == kT192x256 && a_layout != 0) tile = kT256x256;
+  if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
   if (p.part) tile = split256 ? kT256x256 : kT128;
   if (p.drop_mode == 1) return f32 ? launch<0, 0, CULLAVO_DT_F32, 1>(p, s) : launch<0, 0, CULLAVO_DT_BF16, 1>(p, s);
   if (p.drop_mode == 2) {
@@ -1771,6 +1791,11 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     if (a_layout == 1 && b_layout == 0) { L4S(1, 0) }
     L4S(1, 1)
 #undef L4S
+  }
+  if (tile == kT288x256) {  // a_layout 0 (checked above), one loader wave per SIMD
+    if (b_layout == 0)
+      return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
+    return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
   }
   if (tile >= 6) {
     if (a_layout == 0 && b_layout == 0) return launch_alt_ldr<0, 0>(p, tile, f32, s);

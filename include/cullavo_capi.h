@@ -129,9 +129,15 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel
  * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
  * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
- * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers).
+ * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers), 10 = 288x256 /
+ * 8 waves (falls back to 2 when A is not K-contiguous).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
+/* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
+   (its time model: FLOPs / rate x whole rounds of tiles over the CUs); rate <= 0 removes the
+   shape from the automatic choice (0 on mode 10 = round-2 behaviour). *previous (nullable)
+   receives the old rate. Tuning/A-B switch; not thread-safe. */
+int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous);
 /* Stream-K tail of the 8-wave kernels: 0 = off (default; slower on every 7B step shape
    measured), 1 = auto (when a partial last round of tiles would leave >= 25 % of the CUs
    idle), 2 = whenever the last round is partial. The
@@ -260,10 +266,11 @@ size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
    in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */
 int cullavo_attn_set_bwd_tiles(int mode);
-/* A/B switch for the attention forward's K/V tile staging: 1 (default) = 16-B buffer loads
-   whose range check zero-fills rows past the sequence end, 0 = pointer loads behind a per-chunk
-   bounds branch. Results are identical. Synchronous (device symbol copy); returns the previous
-   setting, -1 on a HIP error. */
+/* A/B switch for the attention forward's K/V tile staging: 2 (default) = 16-B buffer loads
+   through a per-tile scalar descriptor (one loop-invariant lane offset, rows past the sequence
+   end zero-filled by the range check), 1 = buffer loads with per-chunk offsets and range selects,
+   0 = pointer loads behind a per-chunk bounds branch. Results are identical. Other values leave
+   the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
    move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in

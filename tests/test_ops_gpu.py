@@ -45,9 +45,9 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, -1],
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 10, -1],
                 ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "t256alt", "t192alt", "t4stage",
-                     "auto"])
+                     "t288x256", "auto"])
 def tile_mode(request):
     from cullavo_amd import _lib
     prev = _lib.lib().cullavo_gemm_set_tile(request.param)
@@ -359,7 +359,8 @@ def test_swiglu():
 
 
 @pytest.mark.parametrize("M,Fd,d,tile", [(8704, 11008, 4096, -1), (1000, 1376, 520, -1), (520, 688, 264, 0),
-                                         (1000, 1376, 520, 2), (1000, 1376, 520, 3), (40, 688, 4104, -1)])
+                                         (1000, 1376, 520, 2), (1000, 1376, 520, 3), (1000, 1376, 520, 10),
+                                         (40, 688, 4104, -1)])
 def test_swiglu_bwd_fused_in_dx_gemm(M, Fd, d, tile):
     """The down-projection dX GEMM with the SwiGLU backward in its epilogue (ACT_SWIGLU_BWD) is
     bitwise equal to dh = dy @ W_down then swiglu_bwd(dh, gu): the 7B shape, ragged tiles, the
@@ -428,7 +429,7 @@ def test_gemm_split256_small_grid(M, N, K, al, bl, epi):
     assert diff.max().item() <= 2 ** -6 * c_ref.float().abs().max().item(), diff.max().item()
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7])
+@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7, 10])
 @pytest.mark.parametrize("al,bl,K", [(0, 0, 1024), (0, 1, 576), (1, 0, 640), (1, 1, 1000), (1, 1, 4096), (0, 0, 1000)])
 def test_gemm_dma_precomputed_offsets_bitwise(tile, al, bl, K):
     """The precomputed-offset LDS-DMA loop (cullavo_gemm_set_dma(1): per-lane source offsets once
@@ -439,8 +440,8 @@ def test_gemm_dma_precomputed_offsets_bitwise(tile, al, bl, K):
     has K % 64 != 0 (K 1000 with al = 0)."""
     from cullavo_amd import _lib
     L = _lib.lib()
-    if tile in (3, 7) and al == 1:
-        pytest.skip("192-row tiles take a layout-0 A only")
+    if tile in (3, 7, 10) and al == 1:
+        pytest.skip("192- and 288-row tiles take a layout-0 A only")
     M, N = 1000, 776
     A = rnd((K, M) if al else (M, K), 90).to(DEV)
     B = rnd((K, N) if bl else (N, K), 91).to(DEV)
@@ -590,6 +591,37 @@ def test_attention_fwd_deferred_rescale_forced(D, causal):
         assert ((lse - outs[0.0][1]).abs() / outs[0.0][1].abs().clamp_min(1.0)).max().item() < 1e-5
     with pytest.raises(ValueError):
         _lib.call("attn_set_rescale", ctypes.c_float(-1.0), None)
+
+
+@pytest.mark.parametrize("B,H,L,D,causal,ks", [(2, 2, 1088, 128, True, [0, 37]), (3, 2, 200, 128, True, [5, 0, 130]),
+                                               (2, 3, 577, 64, False, None), (1, 2, 33, 128, False, None)])
+def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
+    """The forward's K/V staging variants (cullavo_attn_set_stage: 2 = per-tile scalar descriptor,
+    the default; 1 = per-chunk range-checked buffer loads; 0 = pointer loads) stage the same bytes
+    (rows past the sequence end as zeros), so O and LSE are bitwise equal: ragged last tiles
+    (L % 64 != 0), a partial single tile (L = 33), left-padded rows (kv_start), the LM D = 128
+    causal and ViT D = 64 shapes; and the default matches the float reference."""
+    from cullavo_amd import _lib
+    q, k, v = rnd((B * L, H * D), 170), rnd((B * L, H * D), 171), rnd((B * L, H * D), 172)
+    kv = torch.tensor(ks, dtype=torch.int32, device=DEV) if ks is not None else None
+    kw = dict(B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal)
+    if kv is not None:
+        kw["kv_start"] = kv
+    L_ = _lib.lib()
+    outs = {}
+    prev = L_.cullavo_attn_set_stage(2)
+    try:
+        for mode in (2, 1, 0):
+            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2)
+            outs[mode] = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
+    finally:
+        L_.cullavo_attn_set_stage(prev)
+    for mode in (1, 0):
+        assert torch.equal(outs[2][0], outs[mode][0]), f"O differs, stage {mode}"
+        assert torch.equal(outs[2][1], outs[mode][1]), f"LSE differs, stage {mode}"
+    if ks is None:
+        _, _, _, o_ref = _attn_ref(q, k, v, B, H, L, D, causal)
+        close(outs[2][0], o_ref.transpose(1, 2).reshape(B * L, H * D), 1.2e-2, "attn o (stage 2)")
 
 
 @pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
@@ -902,3 +934,43 @@ def test_merge_plan_long_rows_bit_exact(left):
     assert torch.equal(out.cpu().view(B, L, D), r_emb)
     assert torch.equal(mm.cpu(), r_mask.long())
     assert torch.equal(pos.cpu(), r_pos)
+
+
+@pytest.mark.parametrize("M,N,K,bl,epi", [(8704, 4096, 4096, 1, "none"), (8704, 4096, 11008, 0, "res"),
+                                          (1000, 776, 1024, 0, "bias"), (577, 520, 640, 1, "none"),
+                                          (300, 264, 4096, 1, "beta"), (8704, 12288, 4096, 0, "none")])
+def test_gemm_288_rows_bitwise_vs_256(M, N, K, bl, epi):
+    """The 288x256 tile (mode 10: 9 MFMA rows per wave, 36 A pieces over 4 loader waves, 144 KiB
+    LDS epilogue) accumulates every output element over the same K order as the 256x256 tile, so
+    their outputs are bitwise equal: the 7B dX (o_proj) and down-projection forward shapes it is
+    planned for, ragged M (rows past M of the last 288-row tile), K % 64 != 0, accumulate
+    (beta = 1), residual and bias epilogues. Also checks the plan picks it for the 7B dX shape."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    if (M, N, K) == (8704, 4096, 4096):
+        assert L.cullavo_gemm_plan(M, N, K, 0, 1, None) == 10
+    A = rnd((M, K), 95).to(DEV)
+    B = rnd((K, N) if bl else (N, K), 96).to(DEV)
+    bias = rnd((N,), 97).to(DEV) if epi == "bias" else None
+    res = rnd((M, N), 98).to(DEV) if epi == "res" else None
+    beta = 1.0 if epi == "beta" else 0.0
+    C0 = rnd((M, N), 99).to(DEV)
+    outs = {}
+    for tile in (10, 2):
+        prev = L.cullavo_gemm_set_tile(tile)
+        try:
+            C = C0.clone()
+            ops().gemm(0, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, residual=res,
+                       ldr=N if res is not None else 0, beta=beta)
+            torch.cuda.synchronize()
+        finally:
+            L.cullavo_gemm_set_tile(prev)
+        outs[tile] = C
+    assert torch.equal(outs[10], outs[2])
+    if M * N * K <= 2 ** 31:
+        z = A.float() @ (B.float() if bl else B.float().T)
+        if bias is not None:
+            z = z + bias.float()
+        if res is not None:
+            z = z.to(BF).float() + res.float()
+        close(outs[10], z + beta * C0.float(), 8e-3, f"288x256 {M}x{N}x{K}")
