@@ -20,6 +20,7 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 frag8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -94,9 +95,11 @@ DEV frag8 pack_frag(const f32x16& a, int s) {
 constexpr unsigned kOOB = 0x7FFFFFF0u;
 
 __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (cullavo_attn_set_rescale)
-__device__ int g_stage_buf = 1;  // A/B switch (cullavo_attn_set_stage): 0 = pointer loads everywhere
+// forward staging (cullavo_attn_set_stage): 0 = pointer loads behind a bounds branch, 1 = per-chunk
+// range-checked buffer loads, 2 = per-tile descriptor (StageT, the default)
+int g_fwd_stage = 2;
 
-DEV bool buf_ok(int64_t ld, int nrows, int D) { return g_stage_buf && ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
+DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
 
 DEV __amdgpu_buffer_rsrc_t tile_rsrc(const u16* base, int64_t ld, int nrows, int D) {
   const int64_t bytes = nrows > 0 ? ((int64_t)(nrows - 1) * ld + D) * 2 : 0;
@@ -144,13 +147,46 @@ struct Stage {
   }
 };
 
+// Per-tile descriptor staging (the forward's default, STAGE 2): the buffer descriptor is rebuilt
+// per tile from scalars (base advanced to the tile's first row, num_records covering only the
+// rows that exist, so rows past the sequence end read as zeros), every lane keeps ONE
+// loop-invariant byte offset, and the i-th chunk's row step (i * rows-per-pass * ld) is the
+// instruction's scalar offset: no per-tile VALU address arithmetic, compares or selects (the
+// per-chunk form kept 16 v_mul_lo_u32 + range selects in the loop and spilled 62 VGPRs).
+template <int ROWS, int D, int NT = 256>
+struct StageT {
+  static constexpr int kPer = ROWS * D / 8 / NT;  // 16-byte chunks per thread
+  static constexpr int kPass = NT / (D / 8);      // rows covered by one pass of NT threads
+  static_assert(kPer * NT * 8 == ROWS * D && NT % (D / 8) == 0, "tile must split evenly over the threads");
+  u16x8 r[kPer];
+  DEV static unsigned lane_off(int64_t ld) {
+    return (unsigned)(((int64_t)(threadIdx.x / (D / 8)) * ld + (threadIdx.x % (D / 8)) * 8) * 2);
+  }
+  DEV void load(const u16* base, int64_t ld, int row0, int nrows, unsigned vo) {
+    const int left = min(nrows - row0, ROWS);
+    const int bytes = left > 0 ? (int)(((int64_t)(left - 1) * ld + D) * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * ld), (short)0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      r[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (int)(i * kPass * ld * 2), 0));
+  }
+  DEV void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int q = threadIdx.x + NT * i;
+      *reinterpret_cast<u16x8*>(lds + kv_off<D>(q / (D / 8), q % (D / 8))) = r[i];
+    }
+  }
+};
+
 // row of accumulator register r of a 32x32 tile for lane half h
 DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // ============================================================================================
 // forward
 // ============================================================================================
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int STAGE>
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, int64_t ldq,
                                                      const u16* __restrict__ K, int64_t ldk,
                                                      const u16* __restrict__ V, int64_t ldv,
@@ -200,13 +236,27 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   const int ntiles = (kend + KT - 1) / KT;
   const int t0 = kstart / KT;
 
-  Stage<KT, D, true> sk, sv;
+  using St = std::conditional_t<STAGE == 2, StageT<KT, D>, Stage<KT, D, STAGE == 1>>;
+  St sk, sv;
+  unsigned vok = 0, vov = 0;
+  if constexpr (STAGE == 2) {
+    vok = StageT<KT, D>::lane_off(ldk);
+    vov = StageT<KT, D>::lane_off(ldv);
+  }
+  auto load_kv = [&](int row0) {
+    if constexpr (STAGE == 2) {
+      sk.load(Kb, ldk, row0, Lk, vok);
+      sv.load(Vb, ldv, row0, Lk, vov);
+    } else {
+      sk.load(Kb, ldk, row0, Lk);
+      sv.load(Vb, ldv, row0, Lk);
+    }
+  };
   // buffer i: K at smem + 2*i*TILE, V right after it
 #define bufK(i) (smem + 2 * (i) * TILE)
 #define bufV(i) (smem + 2 * (i) * TILE + TILE)
   if (t0 < ntiles) {
-    sk.load(Kb, ldk, t0 * KT, Lk);
-    sv.load(Vb, ldv, t0 * KT, Lk);
+    load_kv(t0 * KT);
     sk.store(bufK(0));
     sv.store(bufV(0));
   }
@@ -220,8 +270,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   // kv_off depends on row & 15 only, so a fragment at row base kb (kb % 16 == 0) sits at the
   // kb = 0 offset plus 2*D*kb (a constant): each read costs one add to the buffer base instead
   // of recomputing the swizzled address.
-  // They are absolute LDS addresses in the current buffer pair (K at 2*cur*TILE, V one TILE
-  // above) and move to the other pair at the end of every tile.
+  // They are absolute LDS addresses in buffer pair 0; the loop body is instantiated once per
+  // buffer pair (CUR = 0 / 1, two tiles per trip), so the pair offset 2*CUR*TILE and every
+  // fragment's row base are compile-time immediates of the ds_read (no per-tile address adds).
   const unsigned sbase = lds_addr(smem);
   unsigned roff[NS];
 #pragma unroll
@@ -236,13 +287,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
       toff[dt][1] = sbase + TILE + kv_off<D>(4 * hf + qq + 8, ch) + 8 * (p & 1);
     }
   }
-  for (int t = t0; t < ntiles; ++t) {
-    const int cur = (t - t0) & 1;
+  const f32x2 c2 = {c, c};
+  auto tile = [&](auto cur_c, int t) {
+    constexpr int CUR = decltype(cur_c)::value;
+    constexpr unsigned PAIR = 2u * CUR * TILE;
     const bool more = t + 1 < ntiles;
-    if (more) {
-      sk.load(Kb, ldk, (t + 1) * KT, Lk);
-      sv.load(Vb, ldv, (t + 1) * KT, Lk);
-    }
+    if (more) load_kv((t + 1) * KT);
     // S^T = K Q^T for two 32-key halves
     f32x16 st[2];
 #pragma unroll
@@ -250,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
       st[kt] = f32x16(0.f);
 #pragma unroll
       for (int s = 0; s < NS; ++s)
-        st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(roff[s] + kt * 32 * 2 * D), qf[s], st[kt], 0, 0, 0);
+        st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(roff[s] + PAIR + kt * 32 * 2 * D), qf[s], st[kt], 0, 0, 0);
     }
     // mask (boundary tiles only, branch-free), tile max on the raw scores (c > 0)
     const int kbase = t * KT;
@@ -273,30 +323,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     // Deferred rescale (cdna_hip_programming.md T13): the reference max m moves -- and O, l are
     // rescaled by exp2(m_old - m_new) -- only on tiles where some row's max grew by more than
     // g_rescale_thr (log2 units); otherwise P = exp2(s c - m) <= 2^thr against the stale m (f32,
-    // and bf16 keeps its relative precision at that scale) and the 64 O multiplies per tile are
-    // skipped. LSE = m + log2(l) is exact either way. thr = 0 rescales whenever a max grows:
-    // bitwise the plain online softmax (a tile that grows no max has alpha = 1 on every lane).
-    float muse;
-    if (__any(tmax > m + rescale_thr)) {  // wave-uniform
-      const float mnew = fmaxf(m, tmax);
-      muse = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = fast_exp2(m - muse);
-      l *= alpha;
+    // and bf16 keeps its relative precision at that scale). LSE = m + log2(l) is exact either
+    // way. thr = 0 rescales whenever a max grows: the plain online softmax. Branch-free: alpha = 1
+    // on tiles that keep the max (a branch around the O multiplies made hipcc reconcile two O
+    // register sets with 64 v_mov_b64 per tile on the common path, more than it skipped).
+    const bool grow = __any(tmax > m + rescale_thr);  // wave-uniform
+    const float mnew = grow ? fmaxf(m, tmax) : m;
+    const float muse = (mnew == -INFINITY) ? 0.f : mnew;
+    const float alpha = grow ? fast_exp2(m - muse) : 1.f;
+    l *= alpha;
 #pragma unroll
-      for (int i = 0; i < ND; ++i) o[i] *= alpha;
-      m = mnew;
-    } else {
-      muse = (m == -INFINITY) ? 0.f : m;
-    }
-    float rs = 0.f;
+    for (int i = 0; i < ND; ++i) o[i] *= alpha;
+    m = mnew;
+    // P = exp2(s c - m): the scale-and-shift and the row sum two lanes' worth at a time
+    // (v_pk_fma_f32 / v_pk_add_f32 on the accumulator's even-aligned register pairs)
+    const f32x2 nm2 = {-muse, -muse};
+    f32x2 rs2 = {0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = fast_exp2(fmaf(st[kt][r], c, -muse));  // exp2(-inf) = 0 for masked keys
-        st[kt][r] = pv;
-        rs += pv;
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 x = {st[kt][r], st[kt][r + 1]};
+        const f32x2 y = __builtin_elementwise_fma(x, c2, nm2);
+        const f32x2 pv = {fast_exp2(y[0]), fast_exp2(y[1])};  // exp2(-inf) = 0 for masked keys
+        st[kt][r] = pv[0];
+        st[kt][r + 1] = pv[1];
+        rs2 += pv;
       }
+    float rs = rs2[0] + rs2[1];
     rs += __shfl_xor(rs, 32, 64);
     l += rs;
     // O^T += V^T P^T
@@ -305,24 +359,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const frag8 pf = pack_frag(st[kt], s);
-        const int vb = (kt * 32 + 16 * s) * 2 * D;
+        const unsigned vb = PAIR + (kt * 32 + 16 * s) * 2 * D;
 #pragma unroll
         for (int dt = 0; dt < ND; ++dt)
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(toff[dt][0] + vb, toff[dt][1] + vb), pf, o[dt], 0, 0, 0);
       }
     if (more) {
-      sk.store(bufK(cur ^ 1));
-      sv.store(bufV(cur ^ 1));
-    }
-    const unsigned step = cur ? -2u * TILE : 2u * TILE;  // to the other buffer pair
-#pragma unroll
-    for (int s = 0; s < NS; ++s) roff[s] += step;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt) {
-      toff[dt][0] += step;
-      toff[dt][1] += step;
+      sk.store(bufK(CUR ^ 1));
+      sv.store(bufV(CUR ^ 1));
     }
     __syncthreads();
+  };
+  for (int t = t0; t < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
   if (q < Lq) {
@@ -727,7 +777,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   const int nqt = (Lq + QT - 1) / QT;
   const bool block_live = kmin < Lk && (kmin + KB > kstart);
 
-  StageN<QT, D, 512> sq, sdo;
+  StageT<QT, D, 512> sq, sdo;  // per-tile descriptors (see StageT)
+  const unsigned voq = StageT<QT, D, 512>::lane_off(ldq), vodo = StageT<QT, D, 512>::lane_off(lddo);
   float aux = 0.f;
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
@@ -745,8 +796,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     skv.load(Vb, ldv, kmin, Lk);
     skv.store(sV);
     if (qt0 < nqt) {
-      sq.load(Qb, ldq, qt0 * QT, Lq);
-      sdo.load(dOb, lddo, qt0 * QT, Lq);
+      sq.load(Qb, ldq, qt0 * QT, Lq, voq);
+      sdo.load(dOb, lddo, qt0 * QT, Lq, vodo);
       sq.store(bufs);
       sdo.store(bufs + TQ);
       load_aux(qt0);
@@ -762,8 +813,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     char* nbuf = bufs + (cur ^ 1) * BUF;
     const bool more = qt + 1 < nqt;
     if (more) {
-      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
-      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
+      sq.load(Qb, ldq, (qt + 1) * QT, Lq, voq);
+      sdo.load(dOb, lddo, (qt + 1) * QT, Lq, vodo);
       load_aux(qt + 1);
     }
     const float* slse = (const float*)(buf + 2 * TQ);
@@ -1207,11 +1258,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
   const int ntiles = (kend + KT - 1) / KT;
   const int t0 = kstart / KT;
 
-  StageN<KT, D, 256> sk;
-  StageN<KT, QB, 256> ss;
+  StageT<KT, D> sk;
+  StageT<KT, QB> ss;
+  const unsigned vok = StageT<KT, D>::lane_off(ldk), vos = StageT<KT, QB>::lane_off(ldst);
   if (t0 < ntiles) {
-    sk.load(Kb, ldk, t0 * KT, Lk);
-    ss.load(Sb, ldst, t0 * KT, LkP);
+    sk.load(Kb, ldk, t0 * KT, Lk, vok);
+    ss.load(Sb, ldst, t0 * KT, LkP, vos);
     sk.store(smem);
     ss.store(smem + TK);
   }
@@ -1222,8 +1274,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
     char* bS = bK + TK;
     const bool more = t + 1 < ntiles;
     if (more) {
-      sk.load(Kb, ldk, (t + 1) * KT, Lk);
-      ss.load(Sb, ldst, (t + 1) * KT, LkP);
+      sk.load(Kb, ldk, (t + 1) * KT, Lk, vok);
+      ss.load(Sb, ldst, (t + 1) * KT, LkP, vos);
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -1267,9 +1319,19 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
                hipStream_t s) {
   const int smem = 4 * 64 * D * 2;
   static bool once = false;
-  if (!once) { set_smem(attn_fwd_k<D, CAUSAL>, smem); once = true; }
+  if (!once) {
+    set_smem(attn_fwd_k<D, CAUSAL, 0>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 1>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 2>, smem);
+    once = true;
+  }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  attn_fwd_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  if (g_fwd_stage == 2)
+    attn_fwd_k<D, CAUSAL, 2><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 1)
+    attn_fwd_k<D, CAUSAL, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else
+    attn_fwd_k<D, CAUSAL, 0><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_fwd");
 }
 
@@ -1384,10 +1446,8 @@ int g_bwd_tiles = -1;
 }  // namespace
 
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
-  int prev = 1;
-  if (hipMemcpyFromSymbol(&prev, HIP_SYMBOL(g_stage_buf), sizeof(int)) != hipSuccess) return -1;
-  const int v = buffer_loads ? 1 : 0;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage_buf), &v, sizeof(int)) != hipSuccess) return -1;
+  const int prev = g_fwd_stage;
+  if (buffer_loads >= 0 && buffer_loads <= 2) g_fwd_stage = buffer_loads;
   return prev;
 }
 
