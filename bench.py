@@ -47,8 +47,10 @@ def parse():
     ap.add_argument("--high-prio", action="store_true",
                     help="run the training step on a high-priority HIP stream (the optimizer's side stream "
                          "stays at the default priority; A/B experiment)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the optimizer update on a side stream under the next forward (A/B; off by default)")
     ap.add_argument("--no-overlap", action="store_true",
-                    help="run the optimizer update in-stream instead of under the next forward (A/B)")
+                    help="optimizer update in-stream (the default; kept for A/B scripts)")
     ap.add_argument("--workload", default="step", choices=["step", "vit"],
                     help="step: the training step (default; configs 3/4/5 by --config/--batch/--text-len); "
                          "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64)")
@@ -279,7 +281,7 @@ def gemm_kernel_name(M, N, K, al=0, bl=0):
     names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0>",
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",
-             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, 1>"}
+             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>"}
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 
@@ -398,7 +400,7 @@ def main():
     opt = {"MODEL": {"CONFIG": args.config}, "LLM": {"TRAINABLE": args.trainable},
            "DATA": {"BATCH_SIZE_PER_GPU": args.batch, "TEXT_LEN": args.text_len, "IMAGE_COL": 35,
                     "STEPS": args.warmup + args.steps},
-           "BUCKET_MB": args.bucket_mb, "OPTIMIZER": {"OVERLAP": not args.no_overlap}}
+           "BUCKET_MB": args.bucket_mb, "OPTIMIZER": {"OVERLAP": args.overlap and not args.no_overlap}}
     tr = CuLLaVO_Trainer(opt)
     rank = tr.accel.process_index
     tr.init_train()

@@ -783,7 +783,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
       const int qq = qt * QT + (int)threadIdx.x % QT;
-      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] * kLog2e : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
     }
   };
   auto store_aux = [&](char* buf) {
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = rr * 4 + j;
-        float pv = fast_exp2(fmaf(sacc[r], c, -l4[j] * kLog2e));
+        float pv = fast_exp2(fmaf(sacc[r], c, -l4[j]));  // lse staged as lse * log2(e)
         if ((unsigned)(qoff + 8 * rr + j) >= qspan) pv = 0.f;
         sacc[r] = pv;
         pacc[r] = pv * (pacc[r] - d4[j]);

@@ -55,6 +55,8 @@ struct GemmArgs {
   int group_m;        // 8-wave tile order: > 0 groups of group_m M-tiles sweep N; < 0 groups of
                       // -group_m N-tiles sweep M
   int dma_pre;        // 8-wave 256-row kernels: per-lane DMA offsets precomputed, K advance in soffset
+  int pf;             // 8-wave 256-row kernels: L2 prefetch of K-tile kt+2 (with dma_pre only)
+  int pf_lds;         // byte offset of the prefetch's dummy LDS slot (past stages and epilogue image)
 };
 
 template <typename V>
@@ -68,6 +70,11 @@ DEV void st_c(const GemmArgs& p, V* dst, const V& v) {
 DEV int img0_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 // layout 1 image: [64 k][128 rows], 32 B unit u of k-row k at unit slot u ^ swz(k)
 DEV int swz1(int k) { return (k & 7) ^ (((k >> 3) & 1) << 2); }
+// position of 16-column unit u in k-row k of a ROWS-wide layout-1 image (an involution): the
+// XOR swizzle within the first 16 units; the 288-wide image's last two units stay in place (its
+// 576-B k-rows already shift by 16 banks per row)
+template <int ROWS>
+DEV int upos(int u, int k) { return (ROWS == 288 && u >= 16) ? u : (u ^ swz1(k)); }
 DEV int img1_off(int k, int unit) { return k * 256 + ((unit ^ swz1(k)) << 5); }
 
 // global -> registers for one 128 x 64 operand tile (4 x 16 B per thread)
@@ -556,11 +563,12 @@ DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t
     constexpr int RB = ROWS * 2;            // bytes per k-row of the image
     constexpr int kPieces = 64 * RB / 1024;
 #pragma unroll
-    for (int i = 0; i < kPieces / NW; ++i) {
+    for (int i = 0; i < (kPieces + NW - 1) / NW; ++i) {
       const int pc = wave + NW * i;
+      if (kPieces % NW != 0 && pc >= kPieces) break;  // wave-uniform
       const int byte = pc * 1024 + lane * 16;
       const int k = byte / RB, b = byte % RB;
-      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+      const int unit = upos<ROWS>(b >> 5, k), half = (b >> 4) & 1;
       const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
       const unsigned off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
@@ -577,11 +585,14 @@ DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t
 // uses it only when K % 64 == 0 for every layout-0 operand.
 constexpr unsigned kOOBp = 0x80000000u;
 
+// pieces per loader wave (ROWS / 8 of them over NW waves; 288 rows over 8 waves: 5 or 4)
+template <int ROWS, int NW>
+constexpr int dma_per() { return (ROWS / 8 + NW - 1) / NW; }
+
 template <int LAYOUT, int ROWS, int NW>
-DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane, unsigned (&vo)[ROWS / 8 / NW]) {
-  static_assert((ROWS / 8) % NW == 0, "LDS-DMA pieces must split evenly over the loader waves");
+DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane, unsigned (&vo)[dma_per<ROWS, NW>()]) {
 #pragma unroll
-  for (int i = 0; i < ROWS / 8 / NW; ++i) {
+  for (int i = 0; i < dma_per<ROWS, NW>(); ++i) {
     const int pc = wave + NW * i;
     int64_t gi, rel;
     if (LAYOUT == 0) {
@@ -593,7 +604,7 @@ DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane,
       constexpr int RB = ROWS * 2;
       const int byte = pc * 1024 + lane * 16;
       const int k = byte / RB, b = byte % RB;
-      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+      const int unit = upos<ROWS>(b >> 5, k), half = (b >> 4) & 1;
       gi = idx0 + unit * 16 + half * 8;
       rel = k * ld + gi;
     }
@@ -604,8 +615,35 @@ DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane,
 template <int ROWS, int NW>
 DEV void dma_issue(__amdgpu_buffer_rsrc_t rsrc, const unsigned* vo, int soff, char* lds, int wave) {
 #pragma unroll
-  for (int i = 0; i < ROWS / 8 / NW; ++i)
+  for (int i = 0; i < dma_per<ROWS, NW>(); ++i) {
+    if ((ROWS / 8) % NW != 0 && wave + NW * i >= ROWS / 8) break;  // wave-uniform
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (wave + NW * i) * 1024), 16, vo[i], soff, 0, 0);
+  }
+}
+
+// L2 prefetch of K-tile kt + 2 (round 3). The 2-stage loop gives each K-tile's LDS-DMA one
+// tile of MFMAs (~2,000 cycles) to land, and the dW / forward panels mostly miss the 4 MB L2
+// (PMC: ~4x the algorithmic bytes come from the Infinity Cache / HBM), so misses sit in the
+// per-tile vmcnt(0). One extra 4-byte-per-lane LDS-DMA per wave touches every 128-B line of
+// the tile two K-steps ahead (A lines on waves 0-3, B lines on waves 4-7; a line per lane),
+// pulling it into L2 a tile early; its data lands in a dummy LDS slot nobody reads, so it
+// needs no register and no ordering, only a counted wait (vmcnt(1) instead of 0: it is the
+// wave's youngest memory operation). Out-of-range rows get kOOBp (dropped by the range check).
+// Lines of a layout-0 operand: one per row (64 k = 128 B); of a layout-1 operand: ROWS*2/128
+// per k-row.
+template <int LAYOUT, int ROWS>
+DEV unsigned pf_prep(int64_t ld, int64_t idx0, int64_t idx_max, int li) {
+  int64_t gi, rel;
+  if (LAYOUT == 0) {
+    gi = idx0 + li;
+    rel = gi * ld;
+  } else {
+    constexpr int LPR = ROWS * 2 / 128;  // lines per k-row
+    const int k = li / LPR, ch = li % LPR;
+    gi = idx0 + ch * 64;
+    rel = (int64_t)k * ld + gi;
+  }
+  return gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
 }
 
 // scalar byte offset of K-tile origin k0 for an operand of layout L
@@ -613,7 +651,7 @@ template <int L>
 DEV int dma_soff(int64_t k0, int64_t ld) { return (int)(L == 0 ? k0 * 2 : k0 * ld * 2); }
 
 template <int ROWS>
-DEV int img1w_off(int k, int unit) { return k * (ROWS * 2) + ((unit ^ swz1(k)) << 5); }
+DEV int img1w_off(int k, int unit) { return k * (ROWS * 2) + (upos<ROWS>(unit, k) << 5); }
 
 // Transposed fragment reads issued by inline asm. The ds_read_tr16 builtin carries no
 // memory-operand info, so hipcc (ROCm 7.2) assumes it may alias the in-flight LDS-DMA of the
@@ -738,9 +776,14 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
     constexpr int NWL = LDR == 0 ? 8 : 4;
     const int lw = LDR == 0 ? wave : (wave & 3);
     const bool loader = LDR == 0 || (LDR == 1 ? wave < 4 : wave >= 4);
-    unsigned va[BM2 / 8 / NWL], vb[BN / 8 / NWL];
+    unsigned va[dma_per<BM2, NWL>()], vb[dma_per<BN, NWL>()];
     dma_prep<AL, BM2, NWL>(p.lda, m0, p.M, lw, lane, va);
     dma_prep<BL, BN, NWL>(p.ldb, n0, p.N, lw, lane, vb);
+    // prefetch lanes: waves 0-3 the first 256 A lines, waves 4-7 the B lines
+    const bool pf_a = wave < 4;
+    const unsigned vpf = pf_a ? pf_prep<AL, BM2>(p.lda, m0, p.M, wave * 64 + lane)
+                              : pf_prep<BL, BN>(p.ldb, n0, p.N, (wave - 4) * 64 + lane);
+    char* pf_slot = smem + p.pf_lds;
     for (int kt = kb; kt < ke; ++kt) {
       char* cur = smem + ((kt - kb) & 1) * STAGE;
       char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
@@ -749,10 +792,23 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
         dma_issue<BM2, NWL>(ra, va, dma_soff<AL>(k1, p.lda), nxt, lw);
         dma_issue<BN, NWL>(rb, vb, dma_soff<BL>(k1, p.ldb), nxt + TILE_A, lw);
       }
+      const bool pf = p.pf && kt + 2 < ke;  // uniform
+      if (pf) {
+        const int64_t k2 = (int64_t)(kt + 2) * BK;
+        if (pf_a) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)pf_slot, 4, vpf, dma_soff<AL>(k2, p.lda), 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)pf_slot, 4, vpf, dma_soff<BL>(k2, p.ldb), 0, 0);
+      }
       tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      // every DMA of tile kt+1 landed; the prefetch (this wave's youngest operation) may fly on.
+      // A raw s_barrier: __syncthreads()'s fence would add vmcnt(0) and wait for the prefetch.
+      if (pf) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
 
@@ -1415,9 +1471,11 @@ int g_splitk_blocks = 512;  // target blocks of a split-K launch (cullavo_gemm_s
 // tile is mostly padding: the register-staged 128x128 split below takes those).
 int num_cus();
 
+// Split over K when the 256x256 grid covers at most half the CUs and K is long (>= 32 K-tiles):
+// e.g. the ViT's fc2 at 8 images (4616 x 1024 x 4096: 76 tiles -> 3 splits, 228 blocks).
 int splitk256_plan(int64_t M, int64_t N, int64_t K, int* kt_per) {
   const int64_t tiles = cdiv(M, 256) * cdiv(N, 256), nk = cdiv(K, BK);
-  if (M < 256 || N < 256 || tiles * 4 > num_cus() || nk < 32) return 1;
+  if (M < 256 || N < 256 || tiles * 2 > num_cus() || nk < 32) return 1;
   int64_t s = std::min<int64_t>(num_cus() / tiles, nk / 8);
   if (s < 2) return 1;
   const int64_t per = cdiv(nk, s);
@@ -1501,8 +1559,10 @@ float* sk_workspace(hipStream_t s) {
 
 template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0>
 int launch256(GemmArgs p, hipStream_t s) {
-  // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB)
-  const int smem = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
+  // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB);
+  // then the prefetch's 256-B dummy slot
+  p.pf_lds = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
+  const int smem = p.pf_lds + 256;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR>,
@@ -1599,6 +1659,10 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   int bid = kT128;
   for (const C& c : cands) {
     if ((c.id == kT192x256 || c.id == kT288x256) && a_layout != 0) continue;
+    // 288 rows only for long K: with 16 K-tiles (the ViT's K = 1024 products) its larger
+    // per-tile prologue and 144 KiB epilogue cost more than the rounds it saves (config 2:
+    // fc1 36928x4096x1024 at 815 TF/s against 865 for the 256-row tile)
+    if (c.id == kT288x256 && K < 2048) continue;
     if (c.rate <= 0.0) continue;
     const int64_t tiles = cdiv(M, c.bm) * cdiv(N, c.bn);
     const double exact = (double)tiles / (double)c.slots;
@@ -1618,6 +1682,11 @@ static int g_force_tile = -1;
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
 static int g_dma_pre = 1;  // +2.7 % on the 7B step (profiles/r03/dma_ab.md)
+// L2 prefetch of K-tile kt+2 in the 8-wave loop (cullavo_gemm_set_prefetch): measured slower on
+// every 7B shape (5-12 %) and on the step (376.9 / 377.4 vs 351.1 / 350.6 ms alternating,
+// profiles/r03/prefetch/): the loop is bound by LDS-DMA issue, not by the data's arrival, so one
+// more memory instruction per wave and K-step costs more than the L2 hits save. Off.
+static int g_prefetch = 0;
 // Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
 // step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
 static int g_group_m = -4;
@@ -1653,6 +1722,12 @@ extern "C" int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previou
   if (previous) *previous = (float)g_tile_rate[i];
   g_tile_rate[i] = tflops > 0.f ? (double)tflops : 0.0;
   return CULLAVO_OK;
+}
+
+extern "C" int cullavo_gemm_set_prefetch(int on) {
+  const int prev = g_prefetch;
+  g_prefetch = on & 1;
+  return prev;
 }
 
 // A/B switch for the precomputed-offset LDS-DMA loop of the 8-wave 256-row kernels
@@ -1749,6 +1824,8 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   }
   p.nt_store = g_nt_store;
   p.dma_pre = g_dma_pre && (a_layout == 1 || K % BK == 0) && (b_layout == 1 || K % BK == 0);
+  p.pf = g_prefetch;
+  p.pf_lds = 0;
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
@@ -1767,6 +1844,8 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     }
   }
   int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
+  // 288-row layout-1 A images do not fit the register budget of the transposed-read kernel
+  // (197 VGPRs spilled): the weight-gradient products keep the 256-row tile
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
   if (p.part) tile = split256 ? kT256x256 : kT128;
   if (p.drop_mode == 1) return f32 ? launch<0, 0, CULLAVO_DT_F32, 1>(p, s) : launch<0, 0, CULLAVO_DT_BF16, 1>(p, s);
@@ -1792,7 +1871,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     L4S(1, 1)
 #undef L4S
   }
-  if (tile == kT288x256) {  // a_layout 0 (checked above), one loader wave per SIMD
+  if (tile == kT288x256) {  // a_layout 0 (above), one loader wave per SIMD
     if (b_layout == 0)
       return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
     return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256, 1>(p, s);

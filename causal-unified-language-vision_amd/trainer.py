@@ -177,9 +177,13 @@ class CuLLaVO_Trainer(DefaultTrainer):
         """reference trainer/cullavo_trainer.py:12-14: AdamW(lr, wd) + CosineAnnealingLR."""
         o = self.opt["OPTIMIZER"]
         cm = self.model.cullavo_model if hasattr(self.model, "cullavo_model") else self.model
-        # OVERLAP: the update runs on a side stream under the next step's forward (optim.py)
+        # OVERLAP: the update runs on a side stream under the next step's forward (optim.py). Off by
+        # default since round 3: the HBM-bound update kernels refill every CU they touch, so the
+        # 8-wave GEMMs (one whole-CU workgroup each) of the next forward starve beside them and
+        # the step gains nothing (config 3: 351.5 / 352.4 ms with, 351.7 / 351.7 without,
+        # alternating on one box; the ViT GEMMs ran at 138 TF/s beside it, 380 without).
         self.optimizer = FusedAdamW(list(cm.arenas.values()), lr=float(o["LR"]), weight_decay=float(o["WEIGHT_DECAY"]),
-                                    overlap=bool(o.get("OVERLAP", True)))
+                                    overlap=bool(o.get("OVERLAP", False)))
         self.lr_scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(
             optimizer=self.optimizer, T_max=max(1, len(self.train_dataloaders) * int(o["EPOCH"])),
             eta_min=float(o["LAST_LR"]))

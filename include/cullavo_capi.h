@@ -130,7 +130,7 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
  * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
  * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers), 10 = 288x256 /
- * 8 waves (falls back to 2 when A is not K-contiguous).
+ * 8 waves (falls back to 2 when A is not K-contiguous; chosen automatically only for K >= 2048).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
@@ -162,9 +162,15 @@ int cullavo_gemm_set_epilogue(int lds_staged);
    or the operand is stored [K][rows], layout 1; the default); 0 = offsets recomputed per
    K-tile. Same results either way. Returns the previous setting. */
 int cullavo_gemm_set_dma(int precomputed);
+/* Tuning/A-B switch for the 8-wave 256-row kernels (with the precomputed-offset loop): 1 =
+   every K-step also touches the 128-B lines of the tile two K-steps ahead (one 4-byte-per-lane
+   LDS-DMA per wave into a dummy LDS slot), so they are L2-resident when their real LDS-DMA is
+   issued; 0 (default: measured 5-12 % slower with it on) = off. Same results either way.
+   Returns the previous setting. */
+int cullavo_gemm_set_prefetch(int on);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
- * 9 = the 8-wave 256x256 kernel split over K (a grid of fewer than half the CUs with >= 8
+ * 9 = the 8-wave 256x256 kernel split over K (a grid of at most half the CUs with >= 32
  * K-tiles, both M and N >= 256): used by cullavo_gemm_ex when the caller passes the workspace
  * cullavo_gemm_workspace() asks for; f32 partials [splits][M][N], reduced in split order
  * (deterministic) with the full epilogue. cullavo_gemm itself (no workspace) never splits. */

@@ -107,13 +107,26 @@ def test_vit_l14_336_encoder_bs64():
         hs = vt.hidden_state(pix, 23)
     torch.cuda.synchronize()
     assert hs.shape == (64, 577, 1024) and torch.isfinite(hs.float()).all()
-    # per-image independence: images 0-1 run alone give the same features as inside the batch
     with torch.no_grad():
         hs2 = vt.hidden_state(pix[:2].contiguous(), 23)
-    assert rel_l2(hs2, hs[:2]) <= 1e-3
+    # per-image independence, bitwise: with every GEMM on one kernel shape (tile 2) images 0-1 run
+    # alone give exactly the features they get inside the batch. (Under the automatic plan the
+    # 2-image fc2, 1154x1024x4096, runs split over K, a different f32 association: 1-ulp bf16
+    # flips that 23 layers amplify to rel-L2 ~1e-2, the accumulation-order floor below.)
+    from cullavo_amd import _lib
+    prev = _lib.lib().cullavo_gemm_set_tile(2)
+    try:
+        with torch.no_grad():
+            hs_t = vt.hidden_state(pix, 23)
+            hs2_t = vt.hidden_state(pix[:2].contiguous(), 23)
+    finally:
+        _lib.lib().cullavo_gemm_set_tile(prev)
+    assert torch.equal(hs2_t, hs_t[:2])
     W = O.to_bf16(Wf)
     ref = O.vision_hidden_states(pix[:2].cpu().to(BF), W, ocfg, 23)[23]
     # 23 layers deep: the bf16 accumulation-order noise floor alone is rel-L2 1.1e-2 here
     # (tools/bf16_noise_floor.py: the oracle against itself with f32-accumulated Linears), so
-    # this gate is 1.5e-2 (measured 1.11e-2) instead of the 1e-2 of the 2-layer models
+    # this gate is 1.5e-2 (measured 1.11e-2) instead of the 1e-2 of the 2-layer models; both the
+    # batch-64 and the 2-image (split-K fc2) runs are held to it
     assert rel_l2(hs[:2], ref) <= 1.5e-2
+    assert rel_l2(hs2, ref) <= 1.5e-2

@@ -936,20 +936,22 @@ def test_merge_plan_long_rows_bit_exact(left):
     assert torch.equal(pos.cpu(), r_pos)
 
 
-@pytest.mark.parametrize("M,N,K,bl,epi", [(8704, 4096, 4096, 1, "none"), (8704, 4096, 11008, 0, "res"),
-                                          (1000, 776, 1024, 0, "bias"), (577, 520, 640, 1, "none"),
-                                          (300, 264, 4096, 1, "beta"), (8704, 12288, 4096, 0, "none")])
-def test_gemm_288_rows_bitwise_vs_256(M, N, K, bl, epi):
-    """The 288x256 tile (mode 10: 9 MFMA rows per wave, 36 A pieces over 4 loader waves, 144 KiB
-    LDS epilogue) accumulates every output element over the same K order as the 256x256 tile, so
-    their outputs are bitwise equal: the 7B dX (o_proj) and down-projection forward shapes it is
-    planned for, ragged M (rows past M of the last 288-row tile), K % 64 != 0, accumulate
-    (beta = 1), residual and bias epilogues. Also checks the plan picks it for the 7B dX shape."""
+@pytest.mark.parametrize("M,N,K,al,bl,epi", [(8704, 4096, 4096, 0, 1, "none"), (8704, 4096, 11008, 0, 0, "res"),
+                                              (1000, 776, 1024, 0, 0, "bias"), (577, 520, 640, 0, 1, "none"),
+                                              (300, 264, 4096, 0, 1, "beta"), (8704, 12288, 4096, 0, 0, "none"),
+                                              (36928, 1024, 4096, 0, 0, "res")])
+def test_gemm_288_rows_bitwise_vs_256(M, N, K, al, bl, epi):
+    """The 288x256 tile (mode 10: 9 MFMA rows per wave, 36 A pieces over the loader waves, 144 KiB
+    LDS epilogue) accumulates every output element over the same K order as the 256x256 tile, so their outputs
+    are bitwise equal: the 7B dX (o_proj) and down-projection forward shapes it is planned for, ragged M (rows past M of the last 288-row tile), K % 64 != 0,
+    accumulate (beta = 1), residual and bias epilogues. Also checks the plan picks it for the 7B
+    dX shape and not for the ViT's K = 1024 products."""
     from cullavo_amd import _lib
     L = _lib.lib()
     if (M, N, K) == (8704, 4096, 4096):
-        assert L.cullavo_gemm_plan(M, N, K, 0, 1, None) == 10
-    A = rnd((M, K), 95).to(DEV)
+        assert L.cullavo_gemm_plan(M, N, K, al, bl, None) == 10
+    assert L.cullavo_gemm_plan(36928, 4096, 1024, 0, 0, None) != 10
+    A = rnd((K, M) if al else (M, K), 95).to(DEV)
     B = rnd((K, N) if bl else (N, K), 96).to(DEV)
     bias = rnd((N,), 97).to(DEV) if epi == "bias" else None
     res = rnd((M, N), 98).to(DEV) if epi == "res" else None
@@ -960,7 +962,7 @@ def test_gemm_288_rows_bitwise_vs_256(M, N, K, bl, epi):
         prev = L.cullavo_gemm_set_tile(tile)
         try:
             C = C0.clone()
-            ops().gemm(0, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, residual=res,
+            ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, residual=res,
                        ldr=N if res is not None else 0, beta=beta)
             torch.cuda.synchronize()
         finally:
@@ -968,9 +970,42 @@ def test_gemm_288_rows_bitwise_vs_256(M, N, K, bl, epi):
         outs[tile] = C
     assert torch.equal(outs[10], outs[2])
     if M * N * K <= 2 ** 31:
-        z = A.float() @ (B.float() if bl else B.float().T)
+        z = (A.float().T if al else A.float()) @ (B.float() if bl else B.float().T)
         if bias is not None:
             z = z + bias.float()
         if res is not None:
             z = z.to(BF).float() + res.float()
         close(outs[10], z + beta * C0.float(), 8e-3, f"288x256 {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("tile", [2, 3, 10, -1])
+@pytest.mark.parametrize("al,bl,M,N,K", [(0, 0, 1000, 776, 1024), (0, 1, 8704, 4096, 4096), (1, 1, 4096, 4096, 8704),
+                                         (1, 1, 1032, 776, 1000), (1, 0, 1000, 776, 640), (0, 0, 4616, 1024, 4096)])
+def test_gemm_l2_prefetch_bitwise(tile, al, bl, M, N, K):
+    """The L2 prefetch of K-tile kt+2 (cullavo_gemm_set_prefetch: a 4-byte LDS-DMA per wave into
+    a dummy slot, the loop's wait vmcnt(1) and a raw barrier) changes no operand: outputs are
+    bitwise equal with it on and off, on every layout pair, ragged edges, a layout-1 K tail, the
+    7B dX / dW shapes and a split-K plan (tile -1 on the ViT fc2 shape at 8 images)."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    if tile in (3, 10) and al == 1:
+        pytest.skip("192- and 288-row tiles take a layout-0 A only")
+    A = rnd((K, M) if al else (M, K), 190).to(DEV)
+    B = rnd((K, N) if bl else (N, K), 191).to(DEV)
+    bias = rnd((N,), 192).to(DEV) if al == 0 else None
+    outs = []
+    prev_t = L.cullavo_gemm_set_tile(tile)
+    try:
+        for mode in (1, 0, 1):
+            prev = L.cullavo_gemm_set_prefetch(mode)
+            C = torch.empty((M, N), dtype=BF, device=DEV)
+            ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias)
+            torch.cuda.synchronize()
+            L.cullavo_gemm_set_prefetch(prev)
+            outs.append(C)
+    finally:
+        L.cullavo_gemm_set_tile(prev_t)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    if M * N * K <= 2 ** 31:
+        z = (A.float().T if al else A.float()) @ (B.float() if bl else B.float().T)
+        close(outs[0], z + (bias.float() if bias is not None else 0), 8e-3, f"prefetch {M}x{N}x{K}")

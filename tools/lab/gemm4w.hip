@@ -16,6 +16,7 @@
 //   3/4/5 stages (tile kt+S issued at step kt: S-1 steps of latency budget)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 typedef unsigned short u16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -65,9 +66,23 @@ DEV void wait_tiles(int n) {
 // sched_group_barrier masks
 constexpr int kMFMA = 0x008, kDSR = 0x100, kDSW = 0x200, kVMR = 0x020;
 
+// Round 3 (ASM variants): the MFMAs as inline asm with the accumulators constrained to AGPRs
+// ("+a"), so hipcc keeps all 256 of them in the accumulator file and the two fragment sets in
+// VGPRs instead of shuffling fragments through AGPRs (364 v_accvgpr moves per 128 MFMAs in the
+// builtin version). Hazards (cdna_hip_programming.md "What hipcc does not do" item 2): the first
+// K-step writes C from the literal 0 (no v_accvgpr_write -> MFMA pair); an accumulate chain on
+// one register tuple needs no wait states; the last MFMAs' results get s_nop 11 (8-pass XDL: 12
+// states) before the compiler's epilogue reads them.
+DEV void mfma_acc(f32x4& c, const frag8& a, const frag8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+DEV void mfma_zero(f32x4& c, const frag8& a, const frag8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
+
 // AB: ablations (results wrong): 1 = no MFMAs (staging + fragment reads only), 2 = no staging
 // (MFMAs + fragment reads of the prologue tiles only)
-template <int V, int S, int IL, int AB = 0>
+template <int V, int S, int IL, int AB = 0, int ASM = 0>
 __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u16* __restrict__ B,
                                               u16* __restrict__ C, int M, int N, int K, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -186,7 +201,8 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
 
   // step kt: MFMAs on tile kt (fragments in cur) with, under them, tile kt+1's fragment reads
   // into nxt and the staging of a later tile. P = kt & 1 (the 2-deep register staging's set).
-  auto step = [&](int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
+  auto step = [&](auto first_c, int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
+    constexpr bool FIRST = decltype(first_c)::value;
     fread(AB == 2 ? (kt & 1) : kt + 1 < nk ? kt + 1 : kt, nxt);
     if constexpr (AB == 2) {
     } else if constexpr (V == 0) {
@@ -201,6 +217,14 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
     if constexpr (AB == 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(cur.a[i]), "v"(cur.b[i]));
+    } else if constexpr (ASM) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if constexpr (FIRST) mfma_zero(acc[i][j], cur.b[j], cur.a[i]);
+          else mfma_acc(acc[i][j], cur.b[j], cur.a[i]);
+        }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -239,12 +263,27 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     __builtin_amdgcn_s_barrier();
   };
+  using T0 = std::false_type;
+  using T1 = std::true_type;
   int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    step(kt, F0, F1, st0);
-    step(kt + 1, F1, F0, st1);
+  if constexpr (ASM) {
+    // K-step 0 peeled (C from 0), then pairs from step 1: step kt reads fragment set kt & 1
+    step(T1{}, 0, F0, F1, st0);
+    kt = 1;
+    for (; kt + 1 < nk; kt += 2) {
+      step(T0{}, kt, F1, F0, st1);
+      step(T0{}, kt + 1, F0, F1, st0);
+    }
+    if (kt < nk) step(T0{}, kt, F1, F0, st1);
+    asm volatile("s_nop 11" : "+a"(acc[7][7]), "+a"(acc[7][6]), "+a"(acc[7][5]), "+a"(acc[7][4]),
+                 "+a"(acc[7][3]), "+a"(acc[7][2]), "+a"(acc[7][1]), "+a"(acc[7][0]));
+  } else {
+    for (; kt + 1 < nk; kt += 2) {
+      step(T0{}, kt, F0, F1, st0);
+      step(T0{}, kt + 1, F1, F0, st1);
+    }
+    if (kt < nk) step(T0{}, kt, F0, F1, st0);
   }
-  if (kt < nk) step(kt, F0, F1, st0);
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -260,16 +299,16 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
   }
 }
 
-template <int V, int S, int IL, int AB = 0>
+template <int V, int S, int IL, int AB = 0, int ASM = 0>
 int launch(int M, int N, int K, const void* A, const void* B, void* C, hipStream_t s) {
   const int smem = S * STAGE;
   static bool set = false;
   if (!set) {
-    (void)hipFuncSetAttribute((const void*)g4w<V, S, IL, AB>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)g4w<V, S, IL, AB, ASM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     set = true;
   }
   const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-  g4w<V, S, IL, AB><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
+  g4w<V, S, IL, AB, ASM><<<tm * tn, 256, smem, s>>>((const u16*)A, (const u16*)B, (u16*)C, M, N, K, tm, tn);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
@@ -290,6 +329,12 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
     case 8: return launch<1, 4, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);   // DMA staging alone (wrong)
     case 9: return launch<2, 3, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);   // register staging alone (wrong)
     case 10: return launch<1, 4, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // MFMA + fragment reads alone (wrong)
+    // round 3: accumulators pinned to AGPRs (inline-asm MFMAs)
+    case 11: return launch<1, 3, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // DMA, 3 stages
+    case 12: return launch<1, 4, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // DMA, 4 stages
+    case 13: return launch<1, 5, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // DMA, 5 stages
+    case 14: return launch<2, 3, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep
+    case 15: return launch<1, 4, 0, 2, 1>((int)M, (int)N, (int)K, A, B, C, s);  // MFMA + fragment reads alone (wrong)
   }
   return 3;
 }
