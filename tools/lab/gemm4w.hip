@@ -201,8 +201,65 @@ __global__ __launch_bounds__(256, 1) void g4w(const u16* __restrict__ A, const u
 
   // step kt: MFMAs on tile kt (fragments in cur) with, under them, tile kt+1's fragment reads
   // into nxt and the staging of a later tile. P = kt & 1 (the 2-deep register staging's set).
+  // ASM == 2: one wave per SIMD has no partner to hide its memory-instruction issue, so the step
+  // spreads it over the MFMAs in program order (volatile asm MFMAs keep their place): before each
+  // group of 8 MFMAs (one accumulator row) the two fragment reads of the next tile's row and one
+  // LDS-DMA piece of tile kt+S
+  auto step_il = [&](auto first_c, int kt, Frags& cur, Frags& nxt) {
+    constexpr bool FIRST = decltype(first_c)::value;
+    const char* rs = smem + ((kt + 1 < nk ? kt + 1 : kt) % S) * STAGE;
+    char* ws = smem + ((kt + S) % S) * STAGE;
+    const int so = (kt + S) * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      nxt.a[i] = *reinterpret_cast<const frag8*>(rs + img(ra_row + i * 16, ch));
+      nxt.b[i] = *reinterpret_cast<const frag8*>(rs + OPB + img(rb_row + i * 16, ch));
+      if (i < 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(ws + lds_w[i]), 16, offA[i], so, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(ws + OPB + lds_w[i - 4]), 16, offB[i - 4], so, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (FIRST) mfma_zero(acc[i][j], cur.b[j], cur.a[i]);
+        else mfma_acc(acc[i][j], cur.b[j], cur.a[i]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    wait_tiles(S - 2);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
+  // ASM == 2 with register staging (V == 2, 2 steps of latency): per group of 8 MFMAs the two
+  // fragment reads, the LDS write of one piece of tile kt+2 (loaded two steps ago) and the global
+  // load of that piece of tile kt+4 into the same registers
+  auto step_il_reg = [&](auto first_c, int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
+    constexpr bool FIRST = decltype(first_c)::value;
+    const char* rs = smem + ((kt + 1 < nk ? kt + 1 : kt) % S) * STAGE;
+    char* ws = smem + ((kt + 2) % S) * STAGE;
+    const int so = (kt + 4) * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      nxt.a[i] = *reinterpret_cast<const frag8*>(rs + img(ra_row + i * 16, ch));
+      nxt.b[i] = *reinterpret_cast<const frag8*>(rs + OPB + img(rb_row + i * 16, ch));
+      *reinterpret_cast<u32x4*>(ws + (i < 4 ? 0 : OPB) + lds_w[i & 3]) = stp[i];
+      stp[i] = __builtin_amdgcn_raw_buffer_load_b128(i < 4 ? ra : rb, i < 4 ? offA[i] : offB[i - 4], so, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (FIRST) mfma_zero(acc[i][j], cur.b[j], cur.a[i]);
+        else mfma_acc(acc[i][j], cur.b[j], cur.a[i]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    __builtin_amdgcn_s_barrier();
+  };
   auto step = [&](auto first_c, int kt, Frags& cur, Frags& nxt, u32x4 (&stp)[8]) {
     constexpr bool FIRST = decltype(first_c)::value;
+    if constexpr (ASM == 2 && V == 2) {
+      step_il_reg(first_c, kt, cur, nxt, stp);
+      return;
+    } else if constexpr (ASM == 2) {
+      step_il(first_c, kt, cur, nxt);
+      return;
+    }
     fread(AB == 2 ? (kt & 1) : kt + 1 < nk ? kt + 1 : kt, nxt);
     if constexpr (AB == 2) {
     } else if constexpr (V == 0) {
@@ -335,6 +392,10 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
     case 13: return launch<1, 5, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // DMA, 5 stages
     case 14: return launch<2, 3, 0, 0, 1>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep
     case 15: return launch<1, 4, 0, 2, 1>((int)M, (int)N, (int)K, A, B, C, s);  // MFMA + fragment reads alone (wrong)
+    case 16: return launch<1, 3, 0, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // DMA 3 stages, interleaved by hand
+    case 17: return launch<1, 4, 0, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // DMA 4 stages, interleaved by hand
+    case 18: return launch<1, 5, 0, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // DMA 5 stages, interleaved by hand
+    case 19: return launch<2, 3, 0, 0, 2>((int)M, (int)N, (int)K, A, B, C, s);  // registers 2-deep, interleaved by hand
   }
   return 3;
 }
