@@ -186,7 +186,7 @@ DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 // ============================================================================================
 // forward
 // ============================================================================================
-template <int D, bool CAUSAL, int STAGE>
+template <int D, bool CAUSAL, int STAGE, int PRIO = 0>
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, int64_t ldq,
                                                      const u16* __restrict__ K, int64_t ldk,
                                                      const u16* __restrict__ V, int64_t ldv,
@@ -293,6 +293,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     constexpr unsigned PAIR = 2u * CUR * TILE;
     const bool more = t + 1 < ntiles;
     if (more) load_kv((t + 1) * KT);
+    // PRIO (A/B, cullavo_attn_set_stage(3)): the two MFMA blocks at raised wave priority, so the
+    // SIMD's other wave (in its softmax) yields the issue slot to the MFMAs (guide T5)
+    if constexpr (PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // S^T = K Q^T for two 32-key halves
     f32x16 st[2];
 #pragma unroll
@@ -301,6 +308,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #pragma unroll
       for (int s = 0; s < NS; ++s)
         st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(roff[s] + PAIR + kt * 32 * 2 * D), qf[s], st[kt], 0, 0, 0);
+    }
+    if constexpr (PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // mask (boundary tiles only, branch-free), tile max on the raw scores (c > 0)
     const int kbase = t * KT;
@@ -354,6 +366,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     rs += __shfl_xor(rs, 32, 64);
     l += rs;
     // O^T += V^T P^T
+    if constexpr (PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -364,6 +381,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
         for (int dt = 0; dt < ND; ++dt)
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(toff[dt][0] + vb, toff[dt][1] + vb), pf, o[dt], 0, 0, 0);
       }
+    if constexpr (PRIO) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (more) {
       sk.store(bufK(CUR ^ 1));
       sv.store(bufV(CUR ^ 1));
@@ -1323,10 +1345,13 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
     set_smem(attn_fwd_k<D, CAUSAL, 0>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 1>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 2>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 2, 1>, smem);
     once = true;
   }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  if (g_fwd_stage == 2)
+  if (g_fwd_stage == 3)
+    attn_fwd_k<D, CAUSAL, 2, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 2)
     attn_fwd_k<D, CAUSAL, 2><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   else if (g_fwd_stage == 1)
     attn_fwd_k<D, CAUSAL, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
@@ -1447,7 +1472,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int prev = g_fwd_stage;
-  if (buffer_loads >= 0 && buffer_loads <= 2) g_fwd_stage = buffer_loads;
+  if (buffer_loads >= 0 && buffer_loads <= 3) g_fwd_stage = buffer_loads;
   return prev;
 }
 

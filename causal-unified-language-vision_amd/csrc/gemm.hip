@@ -1626,6 +1626,8 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
   if constexpr (AL == 0) {
     if (tile == 7)
       return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256, L>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256, L>(p, s);
+    if (tile == 11)  // 288 rows, all eight waves loading (36 A pieces: 5 or 4 per wave)
+      return f32 ? launch256<0, BL, CULLAVO_DT_F32, 288, 256, L>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 288, 256, L>(p, s);
   }
   return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256, L>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256, L>(p, s);
 }
@@ -1711,7 +1713,7 @@ extern "C" int cullavo_gemm_set_streamk(int mode) {
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256) ? mode : -1;
+  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11) ? mode : -1;
   return prev;
 }
 
@@ -1756,9 +1758,9 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   }
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
-  if (tile == 7 && a_layout != 0) tile = 6;
-  static const int bm[11] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288};
-  static const int bn[11] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  if ((tile == 7 || tile == 11) && a_layout != 0) tile = 6;
+  static const int bm[12] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288};
+  static const int bn[12] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;

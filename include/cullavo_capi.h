@@ -130,7 +130,8 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
  * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
  * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers), 10 = 288x256 /
- * 8 waves (falls back to 2 when A is not K-contiguous; chosen automatically only for K >= 2048).
+ * 8 waves (falls back to 2 when A is not K-contiguous; chosen automatically only for K >= 2048),
+ * 11 = mode 10 with the other loader-wave choice (A/B testing).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
@@ -275,8 +276,9 @@ int cullavo_attn_set_bwd_tiles(int mode);
 /* A/B switch for the attention forward's K/V tile staging: 2 (default) = 16-B buffer loads
    through a per-tile scalar descriptor (one loop-invariant lane offset, rows past the sequence
    end zero-filled by the range check), 1 = buffer loads with per-chunk offsets and range selects,
-   0 = pointer loads behind a per-chunk bounds branch. Results are identical. Other values leave
-   the setting; returns the previous setting. Not thread-safe. */
+   0 = pointer loads behind a per-chunk bounds branch, 3 = mode 2 with the two MFMA blocks of a
+   K/V tile at raised wave priority (s_setprio; A/B experiment). Results are identical. Other
+   values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
    move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in

@@ -429,7 +429,7 @@ def test_gemm_split256_small_grid(M, N, K, al, bl, epi):
     assert diff.max().item() <= 2 ** -6 * c_ref.float().abs().max().item(), diff.max().item()
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7, 10])
+@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7, 10, 11])
 @pytest.mark.parametrize("al,bl,K", [(0, 0, 1024), (0, 1, 576), (1, 0, 640), (1, 1, 1000), (1, 1, 4096), (0, 0, 1000)])
 def test_gemm_dma_precomputed_offsets_bitwise(tile, al, bl, K):
     """The precomputed-offset LDS-DMA loop (cullavo_gemm_set_dma(1): per-lane source offsets once
@@ -440,7 +440,7 @@ def test_gemm_dma_precomputed_offsets_bitwise(tile, al, bl, K):
     has K % 64 != 0 (K 1000 with al = 0)."""
     from cullavo_amd import _lib
     L = _lib.lib()
-    if tile in (3, 7, 10) and al == 1:
+    if tile in (3, 7, 10, 11) and al == 1:
         pytest.skip("192- and 288-row tiles take a layout-0 A only")
     M, N = 1000, 776
     A = rnd((K, M) if al else (M, K), 90).to(DEV)
@@ -611,12 +611,12 @@ def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
     outs = {}
     prev = L_.cullavo_attn_set_stage(2)
     try:
-        for mode in (2, 1, 0):
-            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2)
+        for mode in (2, 1, 0, 3):
+            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2, 3)
             outs[mode] = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
     finally:
         L_.cullavo_attn_set_stage(prev)
-    for mode in (1, 0):
+    for mode in (1, 0, 3):
         assert torch.equal(outs[2][0], outs[mode][0]), f"O differs, stage {mode}"
         assert torch.equal(outs[2][1], outs[mode][1]), f"LSE differs, stage {mode}"
     if ks is None:
@@ -958,7 +958,7 @@ def test_gemm_288_rows_bitwise_vs_256(M, N, K, al, bl, epi):
     beta = 1.0 if epi == "beta" else 0.0
     C0 = rnd((M, N), 99).to(DEV)
     outs = {}
-    for tile in (10, 2):
+    for tile in (10, 11, 2):
         prev = L.cullavo_gemm_set_tile(tile)
         try:
             C = C0.clone()
@@ -968,7 +968,7 @@ def test_gemm_288_rows_bitwise_vs_256(M, N, K, al, bl, epi):
         finally:
             L.cullavo_gemm_set_tile(prev)
         outs[tile] = C
-    assert torch.equal(outs[10], outs[2])
+    assert torch.equal(outs[10], outs[2]) and torch.equal(outs[11], outs[2])
     if M * N * K <= 2 ** 31:
         z = (A.float().T if al else A.float()) @ (B.float() if bl else B.float().T)
         if bias is not None:
