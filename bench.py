@@ -277,7 +277,7 @@ def gemm_kernel_name(M, N, K, al=0, bl=0):
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
     tile = _lib.lib().cullavo_gemm_plan(M, N, K, al, bl, ctypes.byref(g))
-    ldr = 1 if al == 0 else 0  # gemm.hip default_ldr
+    ldr = 0 if (al == 1 and os.environ.get("CULLAVO_GEMM_LOADERS") == "1") else 1  # gemm.hip default_ldr
     names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0>",
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",

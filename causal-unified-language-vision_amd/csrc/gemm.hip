@@ -1613,11 +1613,13 @@ int launch256(GemmArgs p, hipStream_t s) {
   return cullavo_check_launch("gemm256");
 }
 
-// Which waves stage the next K-tile, per operand layout (tools/gemm_bench.py, same-run A/B on
-// the model's shapes): with a K-contiguous A one loader wave per SIMD wins 7-14 % (forward and
-// dX products); with both operands read transposed (dW) all eight waves loading wins 10-15 %.
+// Which waves stage the next K-tile (tools/gemm_bench.py, same-run A/B on the model's shapes):
+// one loader wave per SIMD. With a K-contiguous A it won 7-14 % in round 1; for the transposed
+// weight-gradient products all eight waves loading won 10-15 % then, but with the precomputed DMA
+// offsets (round 3) one loader per SIMD is 5-11 % faster there too (tile 6 vs 2 on the five 7B
+// dW shapes, profiles/r03/ldr/gemm_bench.txt).
 template <int AL, int BL>
-constexpr int default_ldr() { return AL == 0 ? 1 : 0; }
+constexpr int default_ldr() { return 1; }
 
 // tile modes 6 / 7: the 256x256 / 192x256 kernels with the other loader choice (A/B testing)
 template <int AL, int BL>
@@ -1689,6 +1691,7 @@ static int g_dma_pre = 1;  // +2.7 % on the 7B step (profiles/r03/dma_ab.md)
 // profiles/r03/prefetch/): the loop is bound by LDS-DMA issue, not by the data's arrival, so one
 // more memory instruction per wave and K-step costs more than the L2 hits save. Off.
 static int g_prefetch = 0;
+static int g_loaders_all = 0;  // cullavo_gemm_set_loaders: 1 = all eight waves load on layout-1 A (dW)
 // Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
 // step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
 static int g_group_m = -4;
@@ -1724,6 +1727,12 @@ extern "C" int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previou
   if (previous) *previous = (float)g_tile_rate[i];
   g_tile_rate[i] = tflops > 0.f ? (double)tflops : 0.0;
   return CULLAVO_OK;
+}
+
+extern "C" int cullavo_gemm_set_loaders(int mode) {
+  const int prev = g_loaders_all;
+  g_loaders_all = mode & 1;
+  return prev;
 }
 
 extern "C" int cullavo_gemm_set_prefetch(int on) {
@@ -1878,6 +1887,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
       return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
     return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
   }
+  if (g_loaders_all && a_layout == 1 && tile == kT256x256) tile = 6;  // A/B: the round-2 dW loader choice
   if (tile >= 6) {
     if (a_layout == 0 && b_layout == 0) return launch_alt_ldr<0, 0>(p, tile, f32, s);
     if (a_layout == 0 && b_layout == 1) return launch_alt_ldr<0, 1>(p, tile, f32, s);

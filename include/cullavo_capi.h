@@ -169,6 +169,11 @@ int cullavo_gemm_set_dma(int precomputed);
    issued; 0 (default: measured 5-12 % slower with it on) = off. Same results either way.
    Returns the previous setting. */
 int cullavo_gemm_set_prefetch(int on);
+/* Tuning/A-B switch for the 8-wave kernels' LDS-DMA loader waves on products with a layout-1 A
+   (the weight gradients): 0 (default) = one loader wave per SIMD, as for every other product;
+   1 = all eight waves load (the round-2 choice, 5-11 % slower with the precomputed offsets).
+   Same results either way. Returns the previous setting. */
+int cullavo_gemm_set_loaders(int mode);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
  * 9 = the 8-wave 256x256 kernel split over K (a grid of at most half the CUs with >= 32

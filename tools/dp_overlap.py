@@ -52,6 +52,7 @@ def main():
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         with tr.accel.accumulate(tr.model):
+            red.enabled = True  # accumulate() re-derives it from the world size (1 here)
             loss = tr.model(batch, tr.accel)["loss_llm"]
             t_bwd0.record()
             loss.backward()  # no finish(): the end of the backward is the overlap window's end
