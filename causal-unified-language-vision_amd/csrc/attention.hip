@@ -96,8 +96,11 @@ constexpr unsigned kOOB = 0x7FFFFFF0u;
 
 __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (cullavo_attn_set_rescale)
 // forward staging (cullavo_attn_set_stage): 0 = pointer loads behind a bounds branch, 1 = per-chunk
-// range-checked buffer loads, 2 = per-tile descriptor (StageT, the default)
-int g_fwd_stage = 2;
+// range-checked buffer loads, 2 = per-tile descriptor (StageT), 3 = 2 + s_setprio, 4 = LDS-DMA
+// (StageDMA, the default since round 3: 138.3 -> 132.0 us on the 7B layer, 153.3 -> 141.9 us on
+// the ViT bs-64 layer, alternating on one MI355X, profiles/r03/s3a/attn_bench.txt), 5 = 4 with
+// inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B)
+int g_fwd_stage = 4;
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
 
@@ -180,8 +183,95 @@ struct StageT {
   }
 };
 
+// LDS-DMA staging of a [ROWS][D] tile (the forward's STAGE 4): buffer_load ... lds writes each
+// 1 KiB piece lane-linearly (lane i -> byte 16 i of the piece), so the kv_off XOR image is
+// produced by permuting the SOURCE chunk: the lane landing in slot s of image row r loads chunk
+// s ^ swizzle(r) (the swizzle is an involution). No staging VGPRs and no ds_write: the data goes
+// HBM/L2 -> LDS directly. Pieces are dealt round-robin over NW waves; the per-lane offsets are
+// loop-invariant (rows relative to the tile origin, which the per-tile descriptor carries, as in
+// StageT: rows past the sequence end fall outside num_records and land as zeros).
+typedef __attribute__((address_space(3))) void lds_void_t;
+// (a free function: the builtin inside a member function made the host pass drop the kernel
+// stubs of every instantiation using it, silently -- undefined symbols at load)
+DEV void lds_dma16(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned vo) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, vo, 0, 0, 0);
+}
+template <int ROWS, int D, int NW>
+struct StageDMA {
+  static constexpr int kRP = 1024 / (2 * D);            // image rows per 1 KiB piece
+  static constexpr int kPieces = ROWS / kRP;
+  static constexpr int kPer = kPieces / NW;             // pieces per wave
+  static_assert(kPer * NW == kPieces, "pieces must split evenly over the waves");
+  unsigned vo[kPer];
+  DEV void prep(int64_t ld, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int pc = wave + NW * i;
+      const int r = pc * kRP + lane / (D / 8), s = lane % (D / 8);
+      const int sw = D == 128 ? (((r & 3) << 2) | ((r >> 2) & 3)) : ((r >> 1) & 7);
+      vo[i] = (unsigned)(((int64_t)r * ld + (s ^ sw) * 8) * 2);
+    }
+  }
+  DEV void issue(const u16* base, int64_t ld, int row0, int nrows, char* lds, int wave) const {
+    const int left = min(nrows - row0, ROWS);
+    const int bytes = left > 0 ? (int)(((int64_t)(left - 1) * ld + D) * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * ld), (short)0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i)
+      lds_dma16(rs, lds + (wave + NW * i) * 1024, vo[i]);
+  }
+};
+
 // row of accumulator register r of a 32x32 tile for lane half h
 DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Forward STAGE 5: the P V^T product's V^T fragments through inline-asm ds_read_b64_tr_b16 (one
+// group = the ND fragments of one 16-key slice, VB the slice's LDS byte offset as an immediate),
+// tied by a counted lgkmcnt wait (CNT = reads allowed to stay in flight: the next group's)
+template <int ND, unsigned VB>
+DEV void tr_group_issue(s16x4 (&lo)[ND], s16x4 (&hi)[ND], const unsigned (&toff)[ND][2]) {
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+                 : "=&v"(lo[dt]), "=&v"(hi[dt])
+                 : "v"(toff[dt][0]), "v"(toff[dt][1]), "n"(VB)
+                 : "memory");
+}
+template <int ND, int CNT>
+DEV void tr_group_tie(s16x4 (&lo)[ND], s16x4 (&hi)[ND]) {
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(lo[dt]), "+v"(hi[dt]) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// Forward STAGE 5, S = K Q^T: 4 K row fragments (k-steps S0..S0+3 at LDS byte offset OFF from
+// each lane's roff) by inline-asm ds_read_b128, tied by a counted lgkmcnt wait
+template <int NS, int S0, unsigned OFF>
+DEV void k_group_issue(s16x8 (&kf)[4], const unsigned (&roff)[NS]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(kf[j]) : "v"(roff[S0 + j]), "n"(OFF) : "memory");
+}
+template <int CNT>
+DEV void k_group_tie(s16x8 (&kf)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int NS, int S0>
+DEV void k_group_mfma(const s16x8 (&kf)[4], const frag8 (&qf)[NS], f32x16& acc) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, kf[j]), qf[S0 + j], acc, 0, 0, 0);
+}
+template <int ND>
+DEV void tr_group_mfma(const s16x4 (&lo)[ND], const s16x4 (&hi)[ND], const frag8& pf, f32x16 (&o)[ND]) {
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) {
+    const s16x8 v = __builtin_shufflevector(lo[dt], hi[dt], 0, 1, 2, 3, 4, 5, 6, 7);
+    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, v), pf, o[dt], 0, 0, 0);
+  }
+}
 
 // ============================================================================================
 // forward
@@ -236,15 +326,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
   const int ntiles = (kend + KT - 1) / KT;
   const int t0 = kstart / KT;
 
-  using St = std::conditional_t<STAGE == 2, StageT<KT, D>, Stage<KT, D, STAGE == 1>>;
+  using St = std::conditional_t<STAGE == 2 || STAGE >= 4, StageT<KT, D>, Stage<KT, D, STAGE == 1>>;
   St sk, sv;
   unsigned vok = 0, vov = 0;
   if constexpr (STAGE == 2) {
     vok = StageT<KT, D>::lane_off(ldk);
     vov = StageT<KT, D>::lane_off(ldv);
   }
+  StageDMA<KT, D, 4> dk_, dv_;
+  if constexpr (STAGE >= 4) {
+    dk_.prep(ldk, __builtin_amdgcn_readfirstlane(wave), lane);
+    dv_.prep(ldv, __builtin_amdgcn_readfirstlane(wave), lane);
+  }
+  // STAGE 4: K and V of the tile at row0 straight into LDS buffer pair i
+  auto dma_kv = [&](int row0, int i) {
+    const int w = __builtin_amdgcn_readfirstlane(wave);
+    dk_.issue(Kb, ldk, row0, Lk, smem + 2 * i * TILE, w);
+    dv_.issue(Vb, ldv, row0, Lk, smem + 2 * i * TILE + TILE, w);
+  };
   auto load_kv = [&](int row0) {
-    if constexpr (STAGE == 2) {
+    if constexpr (STAGE == 2 || STAGE >= 4) {
       sk.load(Kb, ldk, row0, Lk, vok);
       sv.load(Vb, ldv, row0, Lk, vov);
     } else {
@@ -256,9 +357,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #define bufK(i) (smem + 2 * (i) * TILE)
 #define bufV(i) (smem + 2 * (i) * TILE + TILE)
   if (t0 < ntiles) {
-    load_kv(t0 * KT);
-    sk.store(bufK(0));
-    sv.store(bufV(0));
+    if constexpr (STAGE >= 4) {
+      dma_kv(t0 * KT, 0);
+    } else {
+      load_kv(t0 * KT);
+      sk.store(bufK(0));
+      sv.store(bufV(0));
+    }
   }
   // vmcnt(0) the compiler can see on every path: the Q fragments are then known to have
   // landed inside the loop, so the in-loop prefetch of the next K/V tile is not waited for
@@ -292,7 +397,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     constexpr int CUR = decltype(cur_c)::value;
     constexpr unsigned PAIR = 2u * CUR * TILE;
     const bool more = t + 1 < ntiles;
-    if (more) load_kv((t + 1) * KT);
+    if constexpr (STAGE >= 4) {
+      if (more) dma_kv((t + 1) * KT, CUR ^ 1);  // pair CUR^1 was last read before the previous barrier
+    } else {
+      if (more) load_kv((t + 1) * KT);
+    }
     // PRIO (A/B, cullavo_attn_set_stage(3)): the two MFMA blocks at raised wave priority, so the
     // SIMD's other wave (in its softmax) yields the issue slot to the MFMAs (guide T5)
     if constexpr (PRIO) {
@@ -302,12 +411,42 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     }
     // S^T = K Q^T for two 32-key halves
     f32x16 st[2];
+    if constexpr (STAGE == 5) {
+      // K fragments by inline-asm ds_read_b128 in groups of 4, the next group in flight while
+      // the current one's MFMAs issue (hipcc otherwise reads each fragment into one register
+      // quad right before its MFMA, exposing the LDS latency 16 times per tile)
+      st[0] = f32x16(0.f);
+      st[1] = f32x16(0.f);
+      s16x8 ka[4], kb[4];
+      if constexpr (NS == 8) {
+        k_group_issue<NS, 0, PAIR>(ka, roff);
+        k_group_issue<NS, 4, PAIR>(kb, roff);
+        k_group_tie<4>(ka);
+        k_group_mfma<NS, 0>(ka, qf, st[0]);
+        k_group_issue<NS, 0, PAIR + 32 * 2 * D>(ka, roff);
+        k_group_tie<4>(kb);
+        k_group_mfma<NS, 4>(kb, qf, st[0]);
+        k_group_issue<NS, 4, PAIR + 32 * 2 * D>(kb, roff);
+        k_group_tie<4>(ka);
+        k_group_mfma<NS, 0>(ka, qf, st[1]);
+        k_group_tie<0>(kb);
+        k_group_mfma<NS, 4>(kb, qf, st[1]);
+      } else {
+        k_group_issue<NS, 0, PAIR>(ka, roff);
+        k_group_issue<NS, 0, PAIR + 32 * 2 * D>(kb, roff);
+        k_group_tie<4>(ka);
+        k_group_mfma<NS, 0>(ka, qf, st[0]);
+        k_group_tie<0>(kb);
+        k_group_mfma<NS, 0>(kb, qf, st[1]);
+      }
+    } else {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       st[kt] = f32x16(0.f);
 #pragma unroll
       for (int s = 0; s < NS; ++s)
         st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(roff[s] + PAIR + kt * 32 * 2 * D), qf[s], st[kt], 0, 0, 0);
+    }
     }
     if constexpr (PRIO) {
       __builtin_amdgcn_sched_barrier(0);
@@ -371,6 +510,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
       __builtin_amdgcn_s_setprio(1);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (STAGE == 5) {
+      // V^T fragments by inline-asm ds_read_b64_tr_b16 (the builtin carries no memory operand,
+      // so hipcc puts vmcnt(0) -- the next tile's in-flight LDS-DMA -- in front of it), in four
+      // groups of ND fragments, the next group issued before the current one's MFMAs; a counted
+      // lgkmcnt wait ties each group's registers (DS operations complete in order)
+      s16x4 lo0[ND], hi0[ND], lo1[ND], hi1[ND];
+      tr_group_issue<ND, PAIR + 0 * 2 * D>(lo0, hi0, toff);
+      tr_group_issue<ND, PAIR + 16 * 2 * D>(lo1, hi1, toff);
+      tr_group_tie<ND, 2 * ND>(lo0, hi0);
+      tr_group_mfma<ND>(lo0, hi0, pack_frag(st[0], 0), o);
+      tr_group_issue<ND, PAIR + 32 * 2 * D>(lo0, hi0, toff);
+      tr_group_tie<ND, 2 * ND>(lo1, hi1);
+      tr_group_mfma<ND>(lo1, hi1, pack_frag(st[0], 1), o);
+      tr_group_issue<ND, PAIR + 48 * 2 * D>(lo1, hi1, toff);
+      tr_group_tie<ND, 2 * ND>(lo0, hi0);
+      tr_group_mfma<ND>(lo0, hi0, pack_frag(st[1], 0), o);
+      tr_group_tie<ND, 0>(lo1, hi1);
+      tr_group_mfma<ND>(lo1, hi1, pack_frag(st[1], 1), o);
+    } else {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -381,16 +539,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
         for (int dt = 0; dt < ND; ++dt)
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_tr_frag(toff[dt][0] + vb, toff[dt][1] + vb), pf, o[dt], 0, 0, 0);
       }
+    }
     if constexpr (PRIO) {
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (more) {
-      sk.store(bufK(CUR ^ 1));
-      sv.store(bufV(CUR ^ 1));
+    if constexpr (STAGE >= 4) {
+      // the next pair's DMA has landed in LDS (vmcnt counts LDS-DMA), then every wave's
+      // reads of pair CUR are done before anyone overwrites it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      if (more) {
+        sk.store(bufK(CUR ^ 1));
+        sv.store(bufV(CUR ^ 1));
+      }
+      __syncthreads();
     }
-    __syncthreads();
   };
   for (int t = t0; t < ntiles; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);
@@ -1346,10 +1512,16 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
     set_smem(attn_fwd_k<D, CAUSAL, 1>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 2>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 2, 1>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 4>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 5>, smem);
     once = true;
   }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  if (g_fwd_stage == 3)
+  if (g_fwd_stage == 5)
+    attn_fwd_k<D, CAUSAL, 5><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 4)
+    attn_fwd_k<D, CAUSAL, 4><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 3)
     attn_fwd_k<D, CAUSAL, 2, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   else if (g_fwd_stage == 2)
     attn_fwd_k<D, CAUSAL, 2><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
@@ -1472,7 +1644,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int prev = g_fwd_stage;
-  if (buffer_loads >= 0 && buffer_loads <= 3) g_fwd_stage = buffer_loads;
+  if (buffer_loads >= 0 && buffer_loads <= 5) g_fwd_stage = buffer_loads;
   return prev;
 }
 

@@ -278,11 +278,15 @@ size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
    in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */
 int cullavo_attn_set_bwd_tiles(int mode);
-/* A/B switch for the attention forward's K/V tile staging: 2 (default) = 16-B buffer loads
+/* A/B switch for the attention forward's K/V tile staging: 2 = 16-B buffer loads
    through a per-tile scalar descriptor (one loop-invariant lane offset, rows past the sequence
    end zero-filled by the range check), 1 = buffer loads with per-chunk offsets and range selects,
    0 = pointer loads behind a per-chunk bounds branch, 3 = mode 2 with the two MFMA blocks of a
-   K/V tile at raised wave priority (s_setprio; A/B experiment). Results are identical. Other
+   K/V tile at raised wave priority (s_setprio; A/B experiment), 4 (default) = K/V tiles by
+   LDS-DMA (buffer_load ... lds) straight into the swizzled LDS image (no staging registers, no
+   ds_write), 5 = mode 4 with the K and V^T fragment reads as inline-asm groups of 4 under
+   counted lgkmcnt waits (the next group in flight while the current one's MFMAs issue).
+   Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale

@@ -596,8 +596,10 @@ def test_attention_fwd_deferred_rescale_forced(D, causal):
 @pytest.mark.parametrize("B,H,L,D,causal,ks", [(2, 2, 1088, 128, True, [0, 37]), (3, 2, 200, 128, True, [5, 0, 130]),
                                                (2, 3, 577, 64, False, None), (1, 2, 33, 128, False, None)])
 def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
-    """The forward's K/V staging variants (cullavo_attn_set_stage: 2 = per-tile scalar descriptor,
-    the default; 1 = per-chunk range-checked buffer loads; 0 = pointer loads) stage the same bytes
+    """The forward's K/V staging variants (cullavo_attn_set_stage: 2 = per-tile scalar descriptor;
+    1 = per-chunk range-checked buffer loads; 0 = pointer loads; 3 = 2 with raised
+    MFMA priority; 4 = LDS-DMA straight into the swizzled image, the default; 5 = 4 with inline-asm fragment
+    reads in counted groups) stage the same bytes
     (rows past the sequence end as zeros), so O and LSE are bitwise equal: ragged last tiles
     (L % 64 != 0), a partial single tile (L = 33), left-padded rows (kv_start), the LM D = 128
     causal and ViT D = 64 shapes; and the default matches the float reference."""
@@ -611,17 +613,17 @@ def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
     outs = {}
     prev = L_.cullavo_attn_set_stage(2)
     try:
-        for mode in (2, 1, 0, 3):
-            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2, 3)
+        for mode in (2, 1, 0, 3, 4, 5):
+            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2, 3, 4, 5)
             outs[mode] = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
     finally:
         L_.cullavo_attn_set_stage(prev)
-    for mode in (1, 0, 3):
+    for mode in (1, 0, 3, 4, 5):
         assert torch.equal(outs[2][0], outs[mode][0]), f"O differs, stage {mode}"
         assert torch.equal(outs[2][1], outs[mode][1]), f"LSE differs, stage {mode}"
     if ks is None:
         _, _, _, o_ref = _attn_ref(q, k, v, B, H, L, D, causal)
-        close(outs[2][0], o_ref.transpose(1, 2).reshape(B * L, H * D), 1.2e-2, "attn o (stage 2)")
+        close(outs[4][0], o_ref.transpose(1, 2).reshape(B * L, H * D), 1.2e-2, "attn o (stage 4)")
 
 
 @pytest.mark.parametrize("D,causal", [(128, True), (64, False)])

@@ -22,7 +22,7 @@ def timeit(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
-STAGES = [int(x) for x in os.environ.get("ATTN_STAGE_AB", "1").split(",")]  # e.g. 1,0,1,0
+STAGES = [int(x) for x in os.environ.get("ATTN_STAGE_AB", "2").split(",")]  # e.g. 2,4,2,4
 ref_out = {}
 for stage in STAGES:
   if len(STAGES) > 1:
