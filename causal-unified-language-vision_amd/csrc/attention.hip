@@ -101,6 +101,8 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // the ViT bs-64 layer, alternating on one MI355X, profiles/r03/s3a/attn_bench.txt), 5 = 4 with
 // inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B)
 int g_fwd_stage = 4;
+// dK/dV Q / dO staging (cullavo_attn_set_bwd_stage): 0 = registers (StageT), 1 = LDS-DMA
+int g_bwd_stage = 0;
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
 
@@ -918,7 +920,7 @@ struct StageN {
   }
 };
 
-template <int D, bool CAUSAL, bool DS_OUT = false>
+template <int D, bool CAUSAL, bool DS_OUT = false, bool DMA = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
     const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
@@ -940,7 +942,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int kb = lid % nkb, hb = lid / nkb;
   const int h = hb % H, b = hb / H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  // wave index through readfirstlane: wave-uniform to the compiler (scalar slice / half branches
+  // and row bases)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hf = lane >> 5;
   const int ksl = wave & 3, u = wave >> 2;          // 32-key slice, query half of each tile
   const int key = kb * KB + ksl * 32 + (lane & 31);  // this lane's key
   const int kstart = kv_start ? kv_start[b] : 0;
@@ -967,6 +971,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
 
   StageT<QT, D, 512> sq, sdo;  // per-tile descriptors (see StageT)
   const unsigned voq = StageT<QT, D, 512>::lane_off(ldq), vodo = StageT<QT, D, 512>::lane_off(lddo);
+  // DMA (cullavo_attn_set_bwd_stage(1)): Q / dO tiles by LDS-DMA into the swizzled image (as the
+  // forward's StageDMA), no staging registers or ds_write
+  StageDMA<QT, D, 8> dq_, ddo_;
+  if constexpr (DMA) {
+    dq_.prep(ldq, wave, lane);
+    ddo_.prep(lddo, wave, lane);
+  }
   float aux = 0.f;
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
@@ -984,10 +995,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     skv.load(Vb, ldv, kmin, Lk);
     skv.store(sV);
     if (qt0 < nqt) {
-      sq.load(Qb, ldq, qt0 * QT, Lq, voq);
-      sdo.load(dOb, lddo, qt0 * QT, Lq, vodo);
-      sq.store(bufs);
-      sdo.store(bufs + TQ);
+      if constexpr (DMA) {
+        dq_.issue(Qb, ldq, qt0 * QT, Lq, bufs, wave);
+        ddo_.issue(dOb, lddo, qt0 * QT, Lq, bufs + TQ, wave);
+      } else {
+        sq.load(Qb, ldq, qt0 * QT, Lq, voq);
+        sdo.load(dOb, lddo, qt0 * QT, Lq, vodo);
+        sq.store(bufs);
+        sdo.store(bufs + TQ);
+      }
       load_aux(qt0);
       store_aux(bufs);
     }
@@ -1001,8 +1017,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     char* nbuf = bufs + (cur ^ 1) * BUF;
     const bool more = qt + 1 < nqt;
     if (more) {
-      sq.load(Qb, ldq, (qt + 1) * QT, Lq, voq);
-      sdo.load(dOb, lddo, (qt + 1) * QT, Lq, vodo);
+      if constexpr (DMA) {
+        dq_.issue(Qb, ldq, (qt + 1) * QT, Lq, nbuf, wave);  // nbuf was last read before the previous barrier
+        ddo_.issue(dOb, lddo, (qt + 1) * QT, Lq, nbuf + TQ, wave);
+      } else {
+        sq.load(Qb, ldq, (qt + 1) * QT, Lq, voq);
+        sdo.load(dOb, lddo, (qt + 1) * QT, Lq, vodo);
+      }
       load_aux(qt + 1);
     }
     const float* slse = (const float*)(buf + 2 * TQ);
@@ -1049,10 +1070,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
       }
     }
     if (more) {
-      sq.store(nbuf);
-      sdo.store(nbuf + TQ);
+      if constexpr (!DMA) {
+        sq.store(nbuf);
+        sdo.store(nbuf + TQ);
+      }
       store_aux(nbuf);
     }
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's DMA landed
     __syncthreads();
   }
 
@@ -1068,17 +1092,26 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   }
   __syncthreads();
   if (u == 0) {
+    // wave-uniform row base (scalar), one 32-bit lane offset (4 hf rows + column lane & 31);
+    // row r's offset acc_row(r, 0) * ld is scalar too, the column block dt * 32 an immediate:
+    // one saddr store per element instead of 64-bit address arithmetic per element
+    const int k0 = kb * KB + ksl * 32;
+    u16* dKr = dK + ((int64_t)b * Lk + k0) * lddk + (int64_t)h * D;
+    u16* dVr = dV + ((int64_t)b * Lk + k0) * lddv + (int64_t)h * D;
+    const unsigned lk = (unsigned)(4 * hf * lddk + (lane & 31)) * 2u, lv = (unsigned)(4 * hf * lddv + (lane & 31)) * 2u;
+    const int left = Lk - k0;  // rows of this slice that exist (>= 32 on all but the last block)
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
+    for (int r = 0; r < 16; ++r) {
+      if (acc_row(r, hf) < left) {
+        u16* pk = dKr + (int64_t)acc_row(r, 0) * lddk;
+        u16* pv = dVr + (int64_t)acc_row(r, 0) * lddv;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = kb * KB + ksl * 32 + acc_row(r, hf);
-        if (kk < Lk) {
-          const int d = dt * 32 + (lane & 31);
-          dK[((int64_t)b * Lk + kk) * lddk + (int64_t)h * D + d] = f2bf((dk[dt][r] + *slot(0, dt, r)) * scale);
-          dV[((int64_t)b * Lk + kk) * lddv + (int64_t)h * D + d] = f2bf(dv[dt][r] + *slot(1, dt, r));
+        for (int dt = 0; dt < ND; ++dt) {
+          *(u16*)((char*)pk + (lk + dt * 64u)) = f2bf((dk[dt][r] + *slot(0, dt, r)) * scale);
+          *(u16*)((char*)pv + (lv + dt * 64u)) = f2bf(dv[dt][r] + *slot(1, dt, r));
         }
       }
+    }
   }
 }
 
@@ -1572,12 +1605,17 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
   static bool once = false;
   if (!once) {
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL>, smem_a);
+    set_smem(attn_bwd_dkdv8_k<D, CAUSAL, false, true>, smem_a);
     if (DQ8) set_smem(attn_bwd_dq8_k<D, CAUSAL>, smem_b);
     else set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
     once = true;
   }
-  attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
+  if (g_bwd_stage == 1)
+    attn_bwd_dkdv8_k<D, CAUSAL, false, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
+  else
+    attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
   if (DQ8)
     attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
@@ -1600,12 +1638,17 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
   static bool once = false;
   if (!once) {
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true>, smem_a);
+    set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true, true>, smem_a);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
-  attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
+  if (g_bwd_stage == 1)
+    attn_bwd_dkdv8_k<D, CAUSAL, true, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
+  else
+    attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
   attn_bwd_dq_ds_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
       k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
@@ -1645,6 +1688,12 @@ int g_bwd_tiles = -1;
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int prev = g_fwd_stage;
   if (buffer_loads >= 0 && buffer_loads <= 5) g_fwd_stage = buffer_loads;
+  return prev;
+}
+
+extern "C" int cullavo_attn_set_bwd_stage(int mode) {
+  const int prev = g_bwd_stage;
+  if (mode == 0 || mode == 1) g_bwd_stage = mode;
   return prev;
 }
 

@@ -289,6 +289,10 @@ int cullavo_attn_set_bwd_tiles(int mode);
    Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
+/* A/B switch for the backward's 8-wave dK/dV kernel (modes 4, 5, 7): 0 (default) = Q / dO tiles
+   staged through registers and ds_write, 1 = by LDS-DMA straight into the swizzled image.
+   Results are identical. Other values leave the setting; returns the previous one. */
+int cullavo_attn_set_bwd_stage(int mode);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
    move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in
    [0, 16]; default 8: softmax weights stay <= 2^8 against the stale max, LSE exact). 0 = rescale

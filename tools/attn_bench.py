@@ -26,7 +26,8 @@ STAGES = [int(x) for x in os.environ.get("ATTN_STAGE_AB", "2").split(",")]  # e.
 ref_out = {}
 for stage in STAGES:
   if len(STAGES) > 1:
-    _lib.lib().cullavo_attn_set_stage(stage)
+    _lib.lib().cullavo_attn_set_stage(stage % 10)
+    _lib.lib().cullavo_attn_set_bwd_stage(stage // 10)  # e.g. 14 = forward stage 4 + dK/dV DMA
   for name, B, L, H, D, causal in [("LM causal D128", 8, 1088, 32, 128, True), ("ViT D64", 64, 577, 16, 64, False)]:
     torch.manual_seed(0)
     qkv = (torch.randn(B * L, 3 * H * D, device="cuda") * 0.5).bfloat16()
