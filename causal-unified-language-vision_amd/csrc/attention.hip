@@ -101,7 +101,8 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // the ViT bs-64 layer, alternating on one MI355X, profiles/r03/s3a/attn_bench.txt), 5 = 4 with
 // inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B)
 int g_fwd_stage = 4;
-// dK/dV Q / dO staging (cullavo_attn_set_bwd_stage): 0 = registers (StageT), 1 = LDS-DMA
+// backward staging (cullavo_attn_set_bwd_stage): bit 0 = dK/dV Q / dO by LDS-DMA, bit 1 = the
+// dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT)
 int g_bwd_stage = 0;
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
@@ -549,7 +550,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     }
     if constexpr (STAGE >= 4) {
       // the next pair's DMA has landed in LDS (vmcnt counts LDS-DMA), then every wave's
-      // reads of pair CUR are done before anyone overwrites it
+      // reads of pair CUR are done before anyone overwrites it; the sched_barrier keeps the
+      // tile's MFMAs in front of the wait (hipcc otherwise sinks the last ones below it)
+      __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     } else {
@@ -1076,7 +1079,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
       }
       store_aux(nbuf);
     }
-    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's DMA landed
+    if constexpr (DMA) {  // the next tile's DMA landed (MFMAs kept in front of the wait)
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
 
@@ -1449,7 +1455,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w64_k(
 // 64-key tiles up to the causal diagonal with K and dS^T tiles staged in LDS, both operands
 // read as transposed fragments (the same k order on both sides). dS^T has LkP =
 // round_up(Lk, 128) rows (keys) of LqP = round_up(Lq, 128) queries (cullavo_attn_bwd_workspace).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict__ K, int64_t ldk,
                                                            const u16* __restrict__ dST, int64_t ldst, int64_t st_bh,
                                                            int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
@@ -1482,6 +1488,45 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
   StageT<KT, D> sk;
   StageT<KT, QB> ss;
   const unsigned vok = StageT<KT, D>::lane_off(ldk), vos = StageT<KT, QB>::lane_off(ldst);
+  // DMA (cullavo_attn_set_bwd_stage bit 1): K and dS^T tiles by LDS-DMA into the swizzled
+  // images. Every fragment of a tile is read into registers BEFORE the next tile's DMA is issued:
+  // the transposed reads (builtin, no memory operand) would otherwise each wait for that DMA
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  StageDMA<KT, D, 4> dk_;
+  StageDMA<KT, QB, 4> ds_;
+  if constexpr (DMA) {
+    dk_.prep(ldk, wu, lane);
+    ds_.prep(ldst, wu, lane);
+    if (t0 < ntiles) {
+      dk_.issue(Kb, ldk, t0 * KT, Lk, smem, wu);
+      ds_.issue(Sb, ldst, t0 * KT, LkP, smem + TK, wu);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = t0; t < ntiles; ++t) {
+      char* bK = smem + ((t - t0) & 1) * BUF;
+      char* bS = bK + TK;
+      frag8 bsf[NS], kf[NS][ND];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        bsf[s] = tr_frag<QB>(bS, 16 * s, wave * 32, lane);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) kf[s][dt] = tr_frag<D>(bK, 16 * s, dt * 32, lane);
+      }
+      if (t + 1 < ntiles) {  // the other pair was last read before the previous barrier
+        char* nK = smem + ((t - t0 + 1) & 1) * BUF;
+        dk_.issue(Kb, ldk, (t + 1) * KT, Lk, nK, wu);
+        ds_.issue(Sb, ldst, (t + 1) * KT, LkP, nK + TK, wu);
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s][dt], bsf[s], dq[dt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs issue before the wait for the DMA
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
   if (t0 < ntiles) {
     sk.load(Kb, ldk, t0 * KT, Lk, vok);
     ss.load(Sb, ldst, t0 * KT, LkP, vos);
@@ -1511,6 +1556,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
       ss.store(nK + TK);
     }
     __syncthreads();
+  }
   }
   if (q < Lq) {
     u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
@@ -1610,7 +1656,7 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
     else set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
     once = true;
   }
-  if (g_bwd_stage == 1)
+  if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, false, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
   else
@@ -1640,17 +1686,22 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true>, smem_a);
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true, true>, smem_a);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
+    set_smem(attn_bwd_dq_ds_k<D, CAUSAL, true>, smem_b);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
-  if (g_bwd_stage == 1)
+  if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, true, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
   else
     attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
-  attn_bwd_dq_ds_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
-      k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+  if (g_bwd_stage & 2)
+    attn_bwd_dq_ds_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+  else
+    attn_bwd_dq_ds_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
@@ -1693,7 +1744,7 @@ extern "C" int cullavo_attn_set_stage(int buffer_loads) {
 
 extern "C" int cullavo_attn_set_bwd_stage(int mode) {
   const int prev = g_bwd_stage;
-  if (mode == 0 || mode == 1) g_bwd_stage = mode;
+  if (mode >= 0 && mode <= 3) g_bwd_stage = mode;
   return prev;
 }
 

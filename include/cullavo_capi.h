@@ -289,8 +289,9 @@ int cullavo_attn_set_bwd_tiles(int mode);
    Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
-/* A/B switch for the backward's 8-wave dK/dV kernel (modes 4, 5, 7): 0 (default) = Q / dO tiles
-   staged through registers and ds_write, 1 = by LDS-DMA straight into the swizzled image.
+/* A/B switch for the backward's tile staging, two bits: bit 0 = the 8-wave dK/dV kernel's
+   (modes 4, 5, 7) Q / dO tiles, bit 1 = the mode-7 dQ kernel's K / dS^T tiles by LDS-DMA
+   straight into the swizzled image (else through registers and ds_write; 0 = the default).
    Results are identical. Other values leave the setting; returns the previous one. */
 int cullavo_attn_set_bwd_stage(int mode);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale

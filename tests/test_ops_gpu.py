@@ -666,15 +666,18 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
     # mode 7 runs mode 4's dK/dV kernel (plus the dS^T stores): dK, dV bitwise equal to it
     for name, a, b in zip("kv", res8[4][1:], res8[7][1:]):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode 7 vs 4"
-    # the 8-wave dK/dV kernel's LDS-DMA staging of Q / dO (cullavo_attn_set_bwd_stage(1)) stages the
-    # same bytes (rows past Lq as zeros): modes 4 and 7 bitwise equal to the register staging
+    # the LDS-DMA staging (cullavo_attn_set_bwd_stage) stages the same bytes (rows past the end as
+    # zeros): modes 4 and 7 bitwise equal to the register staging, for the dK/dV kernel's Q / dO
+    # (bit 0) and the dQ-from-dS kernel's K / dS^T (bit 1)
     prev_st = _lib.lib().cullavo_attn_set_bwd_stage(1)
     try:
-        for mode8 in (4, 7):
-            _lib.lib().cullavo_attn_set_bwd_tiles(mode8)
-            od = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
-            for name, a, b in zip("qkv", res8[mode8], od):
-                assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode {mode8} DMA staging"
+        for st in (1, 2, 3):
+            _lib.lib().cullavo_attn_set_bwd_stage(st)
+            for mode8 in (4, 7):
+                _lib.lib().cullavo_attn_set_bwd_tiles(mode8)
+                od = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
+                for name, a, b in zip("qkv", res8[mode8], od):
+                    assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode {mode8} DMA staging {st}"
     finally:
         _lib.lib().cullavo_attn_set_bwd_stage(prev_st)
         _lib.lib().cullavo_attn_set_bwd_tiles(prev)
