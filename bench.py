@@ -10,6 +10,12 @@ layers, lm_head + shifted masked CE, the complete backward, bucketed RCCL gradie
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N > 1` without a launcher env (no WORLD_SIZE) starts the N ranks itself, before this process
+touches the GPU: a child `python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1` of this same script (the reference launches its own ranks the same way,
+/root/reference/run:59-71 `accelerate launch --num_processes`); rank 0's JSON line is forwarded
+and the child's exit code returned. A formed world that differs from --gpus is an error (exit 3).
+
 At N = 1 the default run also times the other BASELINE workloads, each in a child process started
 before this process touches the GPU (so their memory never overlaps): config 2 (CLIP ViT-L/14-336
 encoder, bs 64), config 5 (ViT-L + Llama-2-13B, L = 1600, bs 4) and the reference's own recipe on
@@ -32,7 +38,7 @@ sys.path.insert(0, REPO)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -57,7 +63,10 @@ def parse():
     ap.add_argument("--sub-workloads", default=",".join(SUB_WORKLOADS),
                     help="N=1 headline runs only: the other workloads timed in child processes ('' = none)")
     ap.add_argument("--no-sub", action="store_true", help="time this workload only")
-    return ap.parse_args()
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="launcher self-test: form the world, all-reduce one tensor on the host, print one "
+                         "JSON line on rank 0 (no GPU work; tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
 
 
 # the other BASELINE workloads a default N = 1 run reports beside the config-3 headline
@@ -378,10 +387,74 @@ def gemm_ceiling(fam, iters=10):
             "hipblaslt_tflops": round(max(res["hipblaslt"], res["hipblaslt2"]), 1)}
 
 
-def main():
-    args = parse()
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n: int, argv: list[str], port: int) -> list[str]:
+    """the child command that forms an N-rank world on this node (one process per GPU)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def self_launch(n: int, argv: list[str]) -> int:
+    """Start N ranks of this script under torch.distributed.run (this process never touches the
+    GPU), forward rank 0's JSON line to stdout and everything else to stderr; the launcher's exit
+    code is returned (non-zero when any rank failed)."""
+    import subprocess
+    cmd = launch_cmd(n, argv, free_port())
+    print(f"bench.py: --gpus {n} without a launcher env; starting {n} ranks: {' '.join(cmd)}", file=sys.stderr,
+          flush=True)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    json_lines = 0
+    for line in p.stdout:  # rank 0 prints the one JSON line; anything else goes to stderr
+        if line.startswith("{"):
+            json_lines += 1
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    rc = p.wait()
+    if rc == 0 and json_lines != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {json_lines}", file=sys.stderr)
+        return 4
+    return rc
+
+
+def launch_probe(args, world: int) -> None:
+    """--launch-probe: the N>1 launch path without a GPU (world formation, rank env, max-over-ranks
+    reduction, one line on rank 0)."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    if os.environ.get("CULLAVO_PROBE_FAIL_RANK") == str(rank):  # tests: a rank that dies
+        sys.exit(1)
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "launch-probe", "n_gpus": dist.get_world_size(), "gpus_arg": args.gpus,
+                          "max_over_ranks": t.item(), "local_ranks": world}), flush=True)
+    dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
     subs = None
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus, argv))  # before anything touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher formed WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(3)
+    if args.launch_probe:
+        return launch_probe(args, world)
     names = [n for n in args.sub_workloads.split(",") if n]
     if world == 1 and not args.no_sub and args.workload == "step" and names:
         subs = run_sub_workloads(args, names)  # before this process touches the GPU
@@ -395,8 +468,6 @@ def main():
     from cullavo_amd import ops
     from cullavo_amd.trainer import CuLLaVO_Trainer
 
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     opt = {"MODEL": {"CONFIG": args.config}, "LLM": {"TRAINABLE": args.trainable},
            "DATA": {"BATCH_SIZE_PER_GPU": args.batch, "TEXT_LEN": args.text_len, "IMAGE_COL": 35,
                     "STEPS": args.warmup + args.steps},
@@ -430,6 +501,9 @@ def main():
     cfg = cm.config
     T = args.batch * (args.text_len + cfg.vision_config.num_patches - 1)
     ops.trace_gemm("all")
+    reducer = tr.accel.reducer
+    if reducer is not None:
+        reducer.measure = True
 
     if world > 1:
         dist.barrier()
@@ -443,10 +517,24 @@ def main():
     elapsed = time.perf_counter() - t0
     launches = ops.trace_launches()
     fams = gemm_families(launches)
+    exchange = None
     if world > 1:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+        st = reducer.exposure_stats() if reducer is not None else None
+        # the exposed-exchange figure is the slowest rank's too
+        e = torch.tensor([st["exposed_ms"] if st else -1.0, st["host_rendezvous_ms"] if st else -1.0],
+                         device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        exchange = {"backend": dist.get_backend(), "rccl_world_size": dist.get_world_size()
+                    if dist.get_backend() == "nccl" else None, "world_size": dist.get_world_size(),
+                    "allreduce_bytes_per_step": reducer.bytes_per_step if reducer is not None else 0,
+                    "buckets": len(reducer.buckets) if reducer is not None else 0,
+                    "exposed_exchange_ms": round(e[0].item(), 3),
+                    "host_rendezvous_ms": round(e[1].item(), 3),
+                    "exposed_def": "max over ranks of the mean over timed steps: compute stream's backward end "
+                                   "-> all buckets reduced (clip + AdamW may start), HIP events"}
     loss_v = float(loss)
 
     from cullavo_amd.perf import flops_per_sample
@@ -519,6 +607,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)
         if subs is not None:
             line["workloads"] = subs
+        if exchange is not None:
+            line["exchange"] = exchange
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -22,7 +22,8 @@ per step by the fused backward Functions, so a bucket is just a slice of that bu
    the remaining buckets and makes the compute stream wait for the comm stream, so the
    optimizer sees reduced gradients. Mean-of-rank-means = DDP semantics;
  * which keys the optimizer skips is agreed across ranks: a per-key "written on this rank"
-   mask is MAX-reduced over a host (gloo) group, so a key no rank wrote (e.g. the projector
+   mask is MAX-reduced over a host (gloo) group (started asynchronously before the last buckets
+   are issued, waited for after; this is a per-step host rendezvous, not a GPU barrier), so a key no rank wrote (e.g. the projector
    when no rank's batch holds an image) stays skipped exactly as on one GPU (DDP leaves such a
    gradient None and torch AdamW skips it); a key written by any rank gets the averaged
    gradient and a step. The mask is host-side control flow, so the exchange never waits on
@@ -32,10 +33,27 @@ CPU tests) sums and the 1/N scale is applied in finish() after the waits.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
 from .arena import ParamArena
+
+_HOST_GROUPS: dict = {}
+
+
+def host_group(group=None):
+    """A gloo group over the ranks of `group` for the written-key mask, created once per process
+    group (new_group is collective over the default group: every rank of it reaches the first
+    enabled finish() at the same point of the step, so the lazy creation is matched)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group)
+    if key not in _HOST_GROUPS:
+        ranks = dist.get_process_group_ranks(group) if group is not None else None
+        _HOST_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _HOST_GROUPS[key]
 
 
 class GradReducer:
@@ -47,6 +65,7 @@ class GradReducer:
         more than one rank; True runs the exchange at world size 1 too (tests of the RCCL path)."""
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._elem = [ar.flat.element_size() for ar in arenas]
         self.buckets: list[dict] = []
         self._key_bucket: dict[tuple[int, str], int] = {}
         backend = dist.get_backend(group) if dist.is_initialized() else None
@@ -70,16 +89,11 @@ class GradReducer:
         self.stream = torch.cuda.Stream(device=dev) if (use_side_stream and dev.type == "cuda") else None
         self.enabled = self.world > 1 if enabled is None else (bool(enabled) and dist.is_initialized())
         self.timing = None  # a list: record when each bucket becomes ready (overlap analysis)
-        # host group for the written-key mask: the process group itself when it is gloo, else a
-        # gloo group over the same ranks (created collectively here, as every rank builds its
-        # reducer at the same point of init)
-        self._host_group = None
-        if dist.is_initialized():
-            if backend == "gloo":
-                self._host_group = group
-            else:
-                ranks = dist.get_process_group_ranks(group) if group is not None else None
-                self._host_group = dist.new_group(ranks=ranks, backend="gloo")
+        # per finish(): (backward-end event, exchange-done event, host ms in the mask agreement)
+        # on the compute stream when `measure` is set (bench.py's exposed-exchange figure)
+        self.measure = False
+        self.exposure: list[tuple] = []
+        self.bytes_per_step = sum((b["hi"] - b["lo"]) * self._elem[b["arena"]] for b in self.buckets)
         self.reset()
 
     def _add_bucket(self, ai, ar, keys):
@@ -140,12 +154,19 @@ class GradReducer:
         op = dist.ReduceOp.AVG if self.avg_supported else dist.ReduceOp.SUM
         return dist.all_reduce(view, op=op, group=self.group, async_op=True)
 
-    def _agree_skipped(self):
-        """ar.skipped := the keys no rank wrote this cycle (MAX of the per-rank written masks)."""
+    def _start_agree_skipped(self):
+        """Start the MAX of the per-rank written masks on the host group (asynchronous: the
+        buckets are issued while gloo exchanges the mask). This is the exchange's one host
+        rendezvous per step; the GPU never waits on it unless the host falls behind the GPU."""
         keys = [(ar, k) for ar in self.arenas for k in ar.offsets]
         written = torch.tensor([0 if k in ar.skipped else 1 for ar, k in keys], dtype=torch.uint8)
-        if self._host_group is not None or dist.is_initialized():
-            dist.all_reduce(written, op=dist.ReduceOp.MAX, group=self._host_group)
+        work = dist.all_reduce(written, op=dist.ReduceOp.MAX, group=host_group(self.group), async_op=True)
+        return keys, written, work
+
+    def _finish_agree_skipped(self, pending):
+        """ar.skipped := the keys no rank wrote this cycle."""
+        keys, written, work = pending
+        work.wait()
         for ar in self.arenas:
             ar.skipped = set()
         for (ar, k), w in zip(keys, written.tolist()):
@@ -157,13 +178,21 @@ class GradReducer:
         make the current stream wait for all of them (sum backends: scale by 1/N after)."""
         if not self.enabled:
             return
+        cur = torch.cuda.current_stream(self.stream.device) if self.stream is not None else None
+        ev_bwd = None
+        if self.measure and cur is not None:
+            ev_bwd = torch.cuda.Event(enable_timing=True)
+            ev_bwd.record(cur)
         for ar in self.arenas:
             ar.finalize_grads()  # commits the keys it zeroes -> hooks issue their buckets
-        self._agree_skipped()
+        pending = self._start_agree_skipped()
         for b in self.buckets:
             b["pending"].clear()
         self._issue_ready()
         assert self._next == len(self.buckets)
+        t0 = time.perf_counter()
+        self._finish_agree_skipped(pending)
+        host_ms = (time.perf_counter() - t0) * 1e3
         scale = 1.0 / self.world
 
         def _complete():
@@ -175,7 +204,23 @@ class GradReducer:
         if self.stream is not None:
             with torch.cuda.stream(self.stream):
                 _complete()
-            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+            cur.wait_stream(self.stream)
+            if ev_bwd is not None:
+                ev_done = torch.cuda.Event(enable_timing=True)
+                ev_done.record(cur)
+                self.exposure.append((ev_bwd, ev_done, host_ms))
         else:
             _complete()
         self.reset()
+
+    def exposure_stats(self) -> dict | None:
+        """Mean over the measured steps: exposed exchange = backward end (the compute stream's
+        last gradient write) -> the compute stream may start clip + AdamW (all buckets reduced);
+        host_ms = the host time spent waiting for the written-key agreement."""
+        if not self.exposure:
+            return None
+        torch.cuda.synchronize()
+        exp = [a.elapsed_time(b) for a, b, _ in self.exposure]
+        host = [h for _, _, h in self.exposure]
+        return {"exposed_ms": sum(exp) / len(exp), "host_rendezvous_ms": sum(host) / len(host),
+                "steps": len(exp)}

@@ -44,7 +44,10 @@ def _decoder_layer(d, F, H, seed):
     return cfg, ar, layer
 
 
-def _run_decoder_layer(d, F, H, B, L, n_check):
+def _run_decoder_layer(d, F, H, B, L, n_check, samples=None):
+    """n_check: the oracle checks samples 0..n_check-1 (weight gradients too when that is all of
+    them); samples: an explicit list of batch rows checked on the outputs and input gradients
+    instead (e.g. [0, 7] at B = 8: sample 7's rows sit in the ragged last 288-row GEMM tile)."""
     from cullavo_amd.functions import LlamaLayerFn, StepContext
     cfg, ar, layer = _decoder_layer(d, F, H, seed=d)
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -57,18 +60,23 @@ def _run_decoder_layer(d, F, H, B, L, n_check):
     torch.cuda.synchronize()
     assert out.shape == (B * L, d) and torch.isfinite(out.float()).all()
     assert torch.isfinite(h.grad.float()).all() and torch.isfinite(ar.grad_flat.float()).all()
-    # oracle on the first n_check samples, bf16-faithful, same weights and inputs
+    # oracle on the checked samples, bf16-faithful, same weights and inputs
     W = {k: p.detach().cpu().clone().requires_grad_(True) for k, p in ar.params.items()}
     tcfg = O.TextCfg(hidden_size=d, num_hidden_layers=1, num_attention_heads=H, intermediate_size=F)
-    rows = n_check * L
-    hc = h.detach()[:rows].cpu().view(n_check, L, d).clone().requires_grad_(True)
-    cos, sin = O.rope_cos_sin(torch.arange(L)[None].expand(n_check, L), tcfg.head_dim, tcfg.rope_theta)
-    allowed = O.causal_allowed(torch.ones(n_check, L, dtype=torch.long))
+    sel = list(range(n_check)) if samples is None else list(samples)
+    n_sel = len(sel)
+    idx = torch.cat([torch.arange(b * L, (b + 1) * L) for b in sel])
+    rows = n_sel * L
+    hc = h.detach()[idx.cuda()].cpu().view(n_sel, L, d).clone().requires_grad_(True)
+    cos, sin = O.rope_cos_sin(torch.arange(L)[None].expand(n_sel, L), tcfg.head_dim, tcfg.rope_theta)
+    allowed = O.causal_allowed(torch.ones(n_sel, L, dtype=torch.long))
     ref = O.llama_layer(hc, W, "language_model.model.layers.0.", tcfg, cos, sin, allowed)
-    ref.backward(dh3[:rows].cpu().view(n_check, L, d))
-    assert rel_l2(out[:rows], ref.reshape(rows, d)) <= 1e-2
-    assert rel_l2(h.grad[:rows], hc.grad.reshape(rows, d)) <= 2e-2
-    if n_check == B:  # weight gradients sum over every sample: comparable only when all are checked
+    ref.backward(dh3[idx.cuda()].cpu().view(n_sel, L, d))
+    ref = ref.reshape(n_sel, L, d)
+    for j, b in enumerate(sel):  # per sample, so a bad batch row cannot hide behind good ones
+        assert rel_l2(out[b * L:(b + 1) * L], ref[j]) <= 1e-2, f"sample {b} out"
+        assert rel_l2(h.grad[b * L:(b + 1) * L], hc.grad[j]) <= 2e-2, f"sample {b} dX"
+    if samples is None and n_check == B:  # weight gradients sum over every sample: comparable only when all are checked
         for key in ("self_attn.q_proj.weight", "self_attn.o_proj.weight", "mlp.gate_proj.weight",
                     "mlp.down_proj.weight", "input_layernorm.weight"):
             k = "language_model.model.layers.0." + key
@@ -78,6 +86,13 @@ def _run_decoder_layer(d, F, H, B, L, n_check):
 def test_7b_decoder_layer_full_width_L1088():
     """Vicuna-7B decoder layer at the config-3 sequence (576 image + 512 text positions)"""
     _run_decoder_layer(d=4096, F=11008, H=32, B=1, L=1088, n_check=1)
+
+
+def test_7b_decoder_layer_config3_batch8():
+    """Vicuna-7B decoder layer at config 3's real batch (B = 8, L = 1088: M = 8,704 tokens, the
+    288x256 tiles' ragged last M-tile, attention at B*H = 256): samples 0 and 7 against the oracle
+    (reference path: /root/reference/cullavo/arch_cullavo.py:638-665)"""
+    _run_decoder_layer(d=4096, F=11008, H=32, B=8, L=1088, n_check=1, samples=[0, 7])
 
 
 def test_13b_decoder_layer_full_width_L1600_b4():

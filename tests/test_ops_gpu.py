@@ -551,6 +551,38 @@ def test_attention_fwd_bwd(B, H, L, D, causal):
     close(dq, tr(qf.grad), 2e-2, "dq")
 
 
+def test_attention_config3_batch8_sampled_heads():
+    """Attention at config 3's real shape (B = 8, H = 32, L = 1088, D = 128 causal: B*H = 256
+    heads, q|k|v as column blocks of the fused [T, 3d] projection output, the production layout)
+    against the oracle on sampled (batch, head) pairs incl. the last one (b 7, h 31): O, LSE and
+    dQ / dK / dV, same tolerances as test_attention_fwd_bwd (reference path
+    /root/reference/cullavo/arch_cullavo.py:638-665 via the LM's FA2 attention)."""
+    B, H, L, D = 8, 32, 1088, 128
+    hd = H * D
+    qkv = rnd((B * L, 3 * hd), 270).to(DEV)
+    do = rnd((B * L, hd), 271).to(DEV)
+    q, k, v = qkv[:, :hd], qkv[:, hd:2 * hd], qkv[:, 2 * hd:]
+    o, lse = ops().attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=True)
+    dq, dk, dv = ops().attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=True)
+    torch.cuda.synchronize()
+    for t in (o, dq, dk, dv):
+        assert torch.isfinite(t.float()).all()
+    for b, h in ((0, 0), (3, 17), (7, 31), (5, 2)):
+        r, c = slice(b * L, (b + 1) * L), slice(h * D, (h + 1) * D)
+        pick = lambda t: t[r, c].float().cpu().view(1, 1, L, D)
+        qf, kf, vf = (pick(t).requires_grad_(True) for t in (q, k, v))
+        allowed = O.causal_allowed(torch.ones(1, L, dtype=torch.long))
+        o_ref = O.attention(qf, kf, vf, D ** -0.5, allowed)
+        close(o[r, c], o_ref.view(L, D), 1.2e-2, f"o b{b} h{h}")
+        sc = (qf @ kf.transpose(-1, -2)) * D ** -0.5
+        sc = sc.masked_fill(~torch.ones(L, L, dtype=torch.bool).tril(), float("-inf"))
+        close(lse[b, h], torch.logsumexp(sc, -1).view(L), 1e-3, f"lse b{b} h{h}")
+        o_ref.backward(pick(do))
+        close(dq[r, c], qf.grad.view(L, D), 2e-2, f"dq b{b} h{h}")
+        close(dk[r, c], kf.grad.view(L, D), 2e-2, f"dk b{b} h{h}")
+        close(dv[r, c], vf.grad.view(L, D), 2e-2, f"dv b{b} h{h}")
+
+
 @pytest.mark.parametrize("D,causal", [(128, True), (64, False)])
 def test_attention_fwd_deferred_rescale_forced(D, causal):
     """The forward's deferred rescale (cullavo_attn_set_rescale, guide T13 / rule 26): inputs that
@@ -986,13 +1018,22 @@ def test_gemm_288_rows_bitwise_vs_256(M, N, K, al, bl, epi):
             L.cullavo_gemm_set_tile(prev)
         outs[tile] = C
     assert torch.equal(outs[10], outs[2]) and torch.equal(outs[11], outs[2])
-    if M * N * K <= 2 ** 31:
-        z = (A.float().T if al else A.float()) @ (B.float() if bl else B.float().T)
-        if bias is not None:
-            z = z + bias.float()
-        if res is not None:
-            z = z.to(BF).float() + res.float()
-        close(outs[10], z + beta * C0.float(), 8e-3, f"288x256 {M}x{N}x{K}")
+    # fp32 check on sampled rows and columns (every shape, the M = 8,704 ones included): the last
+    # 64 rows (the ragged last 288-row tile at M = 8,704), the first rows and random ones
+    g = torch.Generator().manual_seed(M + N + K)
+    rows = torch.cat([torch.arange(min(64, M)), torch.arange(max(0, M - 64), M),
+                      torch.randint(0, M, (128,), generator=g)]).unique()
+    cols = torch.cat([torch.arange(min(32, N)), torch.arange(max(0, N - 32), N),
+                      torch.randint(0, N, (96,), generator=g)]).unique()
+    Ar = (A.T[rows.to(DEV)] if al else A[rows.to(DEV)]).float().cpu()          # [r, K]
+    Bc = (B.T[cols.to(DEV)] if bl else B[cols.to(DEV)]).float().cpu()          # [c, K]
+    z = Ar @ Bc.T
+    if bias is not None:
+        z = z + bias.float().cpu()[cols]
+    if res is not None:
+        z = z.to(BF).float() + res.float().cpu()[rows][:, cols]
+    z = z + beta * C0.float().cpu()[rows][:, cols]
+    close(outs[10].cpu()[rows][:, cols], z, 8e-3, f"288x256 {M}x{N}x{K} (sampled rows/cols)")
 
 
 @pytest.mark.parametrize("tile", [2, 3, 10, -1])
