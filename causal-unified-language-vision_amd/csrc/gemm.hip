@@ -12,421 +12,16 @@
 //    so each lane ends with 4 consecutive output columns of one row: 8-byte bf16 stores.
 //  * XCD-aware, grouped tile order: consecutive tiles of one XCD share A/B panels in its L2.
 // Epilogue order mirrors the reference's bf16 module chain (see cullavo_capi.h).
-#include "common.h"
+#include "gemm_common.h"
 
 #include <map>
 #include <mutex>
 
+// the ping-pong kernel (tile modes 12 / 13) lives in gemm_pp.hip (its own translation unit)
+int cvgemm_launch_pp(const cvgemm::GemmArgs& p, int ns, int a_layout, int b_layout, bool f32, hipStream_t s);
+
 namespace {
-
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int kTileBytes = 128 * 64 * 2;  // 16 KiB per operand tile
-
-typedef __attribute__((ext_vector_type(8))) __bf16 frag8;
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-struct GemmArgs {
-  const u16* A;
-  const u16* B;
-  void* C;
-  const u16* bias;
-  u16* preact;
-  const u16* residual;
-  int64_t M, N, K, lda, ldb, ldc, ldr;
-  float alpha, beta;
-  int act;
-  int tiles_m, tiles_n;
-  const u16* addend;  // LoRA term added after bias: v = round(round(alpha*AB + bias) + addend)
-  int64_t ld_add;
-  int drop_mode;      // 0 none, 1 A operand, 2 B operand (register-staged kernel), 3 output
-  uint32_t drop_thr;
-  float drop_scale;
-  uint64_t drop_seed;
-  float* part;        // split-K: f32 partials [gridDim.y][M][N] (register-staged kernel only)
-  int kt_per;         // K-tiles per split
-  int epi_lds;        // 8-wave kernels: LDS-staged 16-B epilogue (all pointers 16-B aligned)
-  int nt_store;       // C written with non-temporal stores (streamed past the caches)
-  // stream-K tail of the 8-wave kernels (sk_units = 0: off): blocks < sk_dp run whole tiles;
-  // the sk_units blocks after them split the sk_iters K-iterations of the remaining tiles evenly
-  int sk_dp, sk_units;
-  int64_t sk_iters;
-  float* sk_ws;       // f32 partials [sk_units][2][512 threads x TMW*TN f32x4], fragment order
-  int group_m;        // 8-wave tile order: > 0 groups of group_m M-tiles sweep N; < 0 groups of
-                      // -group_m N-tiles sweep M
-  int dma_pre;        // 8-wave 256-row kernels: per-lane DMA offsets precomputed, K advance in soffset
-  int pf;             // 8-wave 256-row kernels: L2 prefetch of K-tile kt+2 (with dma_pre only)
-  int pf_lds;         // byte offset of the prefetch's dummy LDS slot (past stages and epilogue image)
-};
-
-template <typename V>
-DEV void st_c(const GemmArgs& p, V* dst, const V& v) {
-  if (p.nt_store) __builtin_nontemporal_store(v, dst);
-  else *dst = v;
-}
-
-// ---- LDS images -----------------------------------------------------------------------------
-// layout 0 image: [128 rows][64 k], 16 B chunk c of row r at chunk slot c ^ ((r >> 1) & 7)
-DEV int img0_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
-// layout 1 image: [64 k][128 rows], 32 B unit u of k-row k at unit slot u ^ swz(k)
-DEV int swz1(int k) { return (k & 7) ^ (((k >> 3) & 1) << 2); }
-// position of 16-column unit u in k-row k of a ROWS-wide layout-1 image (an involution): the
-// XOR swizzle within the first 16 units; the 288-wide image's last two units stay in place (its
-// 576-B k-rows already shift by 16 banks per row)
-template <int ROWS>
-DEV int upos(int u, int k) { return (ROWS == 288 && u >= 16) ? u : (u ^ swz1(k)); }
-DEV int img1_off(int k, int unit) { return k * 256 + ((unit ^ swz1(k)) << 5); }
-
-// global -> registers for one 128 x 64 operand tile (4 x 16 B per thread)
-template <int LAYOUT>
-DEV void load_tile(const u16* __restrict__ X, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0,
-                   int64_t K, u16x8 (&r)[4]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = t + 256 * i;
-    if (LAYOUT == 0) {
-      const int row = q >> 3, c = q & 7;
-      const int64_t gi = idx0 + row, gk = k0 + c * 8;
-      r[i] = (gi < idx_max && gk < K) ? *reinterpret_cast<const u16x8*>(X + gi * ld + gk) : u16x8(0);
-    } else {
-      const int k = q >> 4, ch = q & 15;
-      const int64_t gk = k0 + k, gi = idx0 + ch * 8;
-      r[i] = (gk < K && gi < idx_max) ? *reinterpret_cast<const u16x8*>(X + gk * ld + gi) : u16x8(0);
-    }
-  }
-}
-
-template <int LAYOUT>
-DEV void store_tile(char* lds, const u16x8 (&r)[4]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = t + 256 * i;
-    int off;
-    if (LAYOUT == 0) {
-      off = img0_off(q >> 3, q & 7);
-    } else {
-      const int k = q >> 4, ch = q & 15;
-      off = img1_off(k, ch >> 1) + ((ch & 1) << 4);
-    }
-    *reinterpret_cast<u16x8*>(lds + off) = r[i];
-  }
-}
-
-// LoRA dropout on a staged operand tile (the operand is the activation x[token][feature]):
-// layout 0 element (row gi, col gk) is (token gi, feature gk); layout 1 (k-row gk, col gi) is
-// (token gk, feature gi).
-template <int LAYOUT>
-DEV void drop_tile(const GemmArgs& p, int64_t idx0, int64_t k0, u16x8 (&r)[4]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = t + 256 * i;
-    int64_t tok, f0;
-    if (LAYOUT == 0) { tok = idx0 + (q >> 3); f0 = k0 + (q & 7) * 8; }
-    else { tok = k0 + (q >> 4); f0 = idx0 + (q & 15) * 8; }
-    float ms[8];
-    drop_scales<8>(p.drop_seed, p.drop_thr, p.drop_scale, tok, f0, ms);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = bf2f(r[i][j]);
-      r[i][j] = ms[j] != 0.f ? f2bf(v * ms[j]) : (u16)0;
-    }
-  }
-}
-
-// fragment X[idx = rbase + (lane&15)][k = ks*32 + 8*(lane>>4) + j], j = 0..7
-template <int LAYOUT>
-DEV frag8 read_frag(const char* lds, int rbase, int ks, int lane) {
-  if (LAYOUT == 0) {
-    const int row = rbase + (lane & 15);
-    const int c = ks * 4 + (lane >> 4);
-    u16x8 v = *reinterpret_cast<const u16x8*>(lds + img0_off(row, c));
-    return __builtin_bit_cast(frag8, v);
-  } else {
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int unit = rbase >> 4;
-    s16x4 lo, hi;
-    {
-      const int k = ks * 32 + 8 * g + q;
-      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1_off(k, unit) + 8 * p));
-    }
-    {
-      const int k = ks * 32 + 8 * g + 4 + q;
-      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1_off(k, unit) + 8 * p));
-    }
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(frag8, v);
-  }
-}
-
-DEV float act_apply(int act, float x) {
-  if (act == CULLAVO_ACT_GELU) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));  // one op: one rounding
-  if (act == CULLAVO_ACT_QUICK_GELU) {
-    // CLIP quick_gelu x * sigmoid(1.702 x) (tf:activations.py:117-123) as the reference's bf16
-    // tensors evaluate it: the product 1.702 x and the sigmoid each round to bf16, the final
-    // product rounds in the store
-    // exp and reciprocal by the hardware approximations (v_exp_f32, v_rcp_f32: ~1 ulp in f32),
-    // which the bf16 rounding of the sigmoid absorbs except within ~1 ulp of a bf16 tie; the
-    // IEEE division sequence made this epilogue a third of the ViT fc1 GEMM
-    // (tools/vit_gemm_bench.py)
-    const float t = round_bf(1.702f * x);
-    const float e = __builtin_amdgcn_exp2f(t * -1.4426950408889634f);
-    const float sg = round_bf(__builtin_amdgcn_rcpf(1.f + e));
-    return sg * x;
-  }
-  return x;
-}
-
-// quick_gelu of act_apply on 8 values, two at a time: the products and the sum as packed f32
-// (v_pk_mul_f32 / v_pk_add_f32) and both bf16 roundings as one v_cvt_pk_bf16_f32 per pair; the
-// same operations in the same order as act_apply, so bit-identical (the epilogue of the ViT fc1
-// GEMM, where the activation was ~30 % of the GEMM's time, tools/vit_gemm_bench.py)
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-DEV f32x2v round_bf2(f32x2v x) {
-  const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2v));
-  return f32x2v{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
-}
-DEV void quick_gelu8(float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const f32x2v x = {v[j], v[j + 1]};
-    const f32x2v t = round_bf2(1.702f * x);
-    const f32x2v a = t * -1.4426950408889634f;
-    const f32x2v d = 1.f + f32x2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-    const f32x2v sg = round_bf2(f32x2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)});
-    const f32x2v y = sg * x;
-    v[j] = y.x;
-    v[j + 1] = y.y;
-  }
-}
-
-// bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
-DEV int xcd_remap(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-}
-
-// CULLAVO_ACT_SWIGLU_BWD epilogue for NV consecutive columns: the product is dh = d(silu(g) * u)
-// of the SwiGLU, rounded to bf16 as the unfused path stores it; with g = gu[m][n], u = gu[m][F + n]
-// (gu = p.residual, F = p.N) it writes dg to C[m][n] and du to C[m][F + n], in the arithmetic of
-// swiglu_bwd_k (elementwise.hip) so the fused and unfused paths are bitwise equal.
-DEV float sigmoid_ieee(float x) { return 1.f / (1.f + __expf(-x)); }
-
-template <int NV>
-DEV void swiglu_bwd_store(const GemmArgs& p, const float* acc, int64_t m, int64_t n) {
-  typedef __attribute__((ext_vector_type(NV))) unsigned short uv_t;
-  const u16* gr = p.residual + m * p.ldr;
-  const uv_t gv = *reinterpret_cast<const uv_t*>(gr + n);
-  const uv_t uv = *reinterpret_cast<const uv_t*>(gr + p.N + n);
-  uv_t oa, ob;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const float dv = round_bf(acc[j] * p.alpha);
-    const float g = bf2f(gv[j]), u = bf2f(uv[j]);
-    const float sg = sigmoid_ieee(g);
-    const float silu = g * sg;
-    ob[j] = f2bf(dv * round_bf(silu));
-    oa[j] = f2bf(dv * u * sg * (1.f + g * (1.f - sg)));
-  }
-  u16* cp = (u16*)p.C + m * p.ldc + n;
-  *reinterpret_cast<uv_t*>(cp) = oa;
-  *reinterpret_cast<uv_t*>(cp + p.N) = ob;
-}
-
-// epilogue for one lane's C[m][n .. n+3] (bias -> preact -> act -> residual -> beta -> store)
-template <int CT>
-DEV void store4(const GemmArgs& p, const f32x4& acc, int64_t m, int64_t n) {
-  if (m >= p.M || n >= p.N) return;
-  if (CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD) {
-    const float a[4] = {acc[0], acc[1], acc[2], acc[3]};
-    swiglu_bwd_store<4>(p, a, m, n);
-    return;
-  }
-  float v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = acc[j] * p.alpha;
-  if (p.drop_mode == 3) {
-    float ms[4];
-    drop_scales<4>(p.drop_seed, p.drop_thr, p.drop_scale, m, n, ms);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = ms[j] != 0.f ? v[j] * ms[j] : 0.f;
-  }
-  if (p.bias) {
-    const u16x4 bv = *reinterpret_cast<const u16x4*>(p.bias + n);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += bf2f(bv[j]);
-  }
-  if (p.addend) {
-    const u16x4 av = *reinterpret_cast<const u16x4*>(p.addend + m * p.ld_add + n);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(av[j]);
-  }
-  if (p.act != CULLAVO_ACT_NONE || p.preact) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]);
-    if (p.preact) {
-      u16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-      *reinterpret_cast<u16x4*>(p.preact + m * p.ldc + n) = o;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = act_apply(p.act, v[j]);
-  }
-  if (p.residual) {
-    const u16x4 rv = *reinterpret_cast<const u16x4*>(p.residual + m * p.ldr + n);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
-  }
-  if (CT == CULLAVO_DT_BF16) {
-    u16* cp = (u16*)p.C + m * p.ldc + n;
-    if (p.beta != 0.f) {
-      const u16x4 old = *reinterpret_cast<const u16x4*>(cp);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] += p.beta * bf2f(old[j]);
-    }
-    u16x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
-    st_c(p, reinterpret_cast<u16x4*>(cp), o);
-  } else {
-    float* cp = (float*)p.C + m * p.ldc + n;
-    f32x4 o;
-    if (p.beta != 0.f) {
-      const f32x4 old = *reinterpret_cast<const f32x4*>(cp);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = v[j] + p.beta * old[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = v[j];
-    }
-    st_c(p, reinterpret_cast<f32x4*>(cp), o);
-  }
-}
-
-// the same epilogue for 8 consecutive columns C[m][n .. n+7] with 16-B accesses (the
-// LDS-staged path below; every pointer 16-B aligned and every ld a multiple of 8, see
-// lds_epi_ok)
-template <int CT>
-DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
-  if (m >= p.M || n >= p.N) return;  // N % 8 == 0: the whole group is in range
-  if (CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD) {
-    swiglu_bwd_store<8>(p, a, m, n);
-    return;
-  }
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = a[j] * p.alpha;
-  if (p.drop_mode == 3) {
-    float ms[8];
-    drop_scales<8>(p.drop_seed, p.drop_thr, p.drop_scale, m, n, ms);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = ms[j] != 0.f ? v[j] * ms[j] : 0.f;
-  }
-  if (p.bias) {
-    const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += bf2f(bv[j]);
-  }
-  if (p.addend) {
-    const u16x8 av = *reinterpret_cast<const u16x8*>(p.addend + m * p.ld_add + n);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) + bf2f(av[j]);
-  }
-  if (p.act != CULLAVO_ACT_NONE || p.preact) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]);
-    if (p.preact) {
-      u16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-      *reinterpret_cast<u16x8*>(p.preact + m * p.ldc + n) = o;
-    }
-    if (p.act == CULLAVO_ACT_QUICK_GELU) {
-      quick_gelu8(v);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
-    }
-  }
-  if (p.residual) {
-    const u16x8 rv = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) + bf2f(rv[j]);
-  }
-  if (CT == CULLAVO_DT_BF16) {
-    u16* cp = (u16*)p.C + m * p.ldc + n;
-    if (p.beta != 0.f) {
-      const u16x8 old = *reinterpret_cast<const u16x8*>(cp);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += p.beta * bf2f(old[j]);
-    }
-    u16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-    st_c(p, reinterpret_cast<u16x8*>(cp), o);
-  } else {
-    float* cp = (float*)p.C + m * p.ldc + n;
-    f32x4 o0, o1;
-    if (p.beta != 0.f) {
-      const f32x4 q0 = *reinterpret_cast<const f32x4*>(cp), q1 = *reinterpret_cast<const f32x4*>(cp + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { o0[j] = v[j] + p.beta * q0[j]; o1[j] = v[4 + j] + p.beta * q1[j]; }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { o0[j] = v[j]; o1[j] = v[4 + j]; }
-    }
-    st_c(p, reinterpret_cast<f32x4*>(cp), o0);
-    st_c(p, reinterpret_cast<f32x4*>(cp + 4), o1);
-  }
-}
-
-// LDS-staged epilogue of the 8-wave kernels (256-column tiles): per row half (wave row wm),
-// the owning waves write their f32 accumulators into a [BM/2][256] image (16-B chunk c of row
-// r at chunk c ^ (r & 15): conflict-free ds_write_b128), then all 512 threads run store8 on
-// 8 contiguous columns each, so every global access is a full-width 16-B access and 32 lanes
-// cover one 512-B output row (the per-lane 8-B stores of the MFMA layout touch 16 rows per
-// instruction; measured +3-4 % on the whole GEMM, tools/lab/gemm_lab.hip).
-template <int CT, int BM2, int TMW, int TN>
-DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wm,
-                      int wn, int lane) {
-  static_assert(TN == 4, "256-column tiles");
-  constexpr int R = BM2 / 2;
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wm == half) {
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          const int r = tm * 16 + (lane & 15);
-          const int c = wn * 16 + tn * 4 + (lane >> 4);
-          *reinterpret_cast<f32x4*>(smem + r * 1024 + ((c ^ (r & 15)) << 4)) = acc[tm][tn];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < R * 32 / 512; ++i) {
-      const int idx = threadIdx.x + 512 * i;
-      const int r = idx >> 5, pr = idx & 31;
-      const int sw = (pr >> 3) & 1;  // odd chunk first for pairs 8-15, 24-31: conflict-free reads
-      const int c0 = 2 * pr + sw, c1 = 2 * pr + 1 - sw;
-      const char* rowp = smem + r * 1024;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(rowp + ((c0 ^ (r & 15)) << 4));
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(rowp + ((c1 ^ (r & 15)) << 4));
-      const f32x4 lo = sw ? x1 : x0, hi = sw ? x0 : x1;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-      store8<CT>(p, v, m0 + half * R + r, n0 + pr * 8);
-    }
-    __syncthreads();
-  }
-}
+using namespace cvgemm;
 
 template <int AL, int BL, int CT, int DROP = 0>
 __global__ __launch_bounds__(256, 2) void gemm_k(GemmArgs p) {
@@ -526,338 +121,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs p, int splits) {
     for (int s = 0; s < splits; ++s) acc += *reinterpret_cast<const f32x4*>(p.part + ((int64_t)s * p.M + m) * p.N + n);
     store4<CT>(p, acc, m, n);
   }
-}
-
-// ============================================================================================
-// 256-row tile, 8 waves, operands streamed by LDS-DMA (buffer_load ... lds)
-// ============================================================================================
-// Every 1 KiB LDS-DMA wave-instruction writes lane-linearly, so the XOR-swizzled LDS images
-// above are produced by permuting each lane's SOURCE address (cdna_hip_programming.md rule
-// 21). Out-of-range rows / K tails are zero-filled by the buffer range check: such lanes get
-// an offset past num_records.
-constexpr unsigned kOOB = 0x7FFFFFF0u;
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-DEV __amdgpu_buffer_rsrc_t make_rsrc(const u16* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
-}
-
-// fill one [ROWS][64] (layout 0) or [64][ROWS] (layout 1) operand image; NW waves share it
-template <int LAYOUT, int ROWS, int NW>
-DEV void dma_tile(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
-                  char* lds, int wave, int lane) {
-  if (LAYOUT == 0) {
-    constexpr int kPieces = ROWS / 8;  // 8 rows of 128 B per 1 KiB piece
-#pragma unroll
-    for (int i = 0; i < (kPieces + NW - 1) / NW; ++i) {
-      const int pc = wave + NW * i;
-      if (kPieces % NW != 0 && pc >= kPieces) break;  // 288 rows = 36 pieces over 8 waves (wave-uniform)
-      const int row = pc * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
-      const unsigned off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
-    }
-  } else {
-    constexpr int RB = ROWS * 2;            // bytes per k-row of the image
-    constexpr int kPieces = 64 * RB / 1024;
-#pragma unroll
-    for (int i = 0; i < (kPieces + NW - 1) / NW; ++i) {
-      const int pc = wave + NW * i;
-      if (kPieces % NW != 0 && pc >= kPieces) break;  // wave-uniform
-      const int byte = pc * 1024 + lane * 16;
-      const int k = byte / RB, b = byte % RB;
-      const int unit = upos<ROWS>(b >> 5, k), half = (b >> 4) & 1;
-      const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
-      const unsigned off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
-    }
-  }
-}
-
-// Same pieces with the per-lane source offsets computed once per tile (dma_prep) and the K
-// advance passed as the instruction's scalar offset (dma_issue): a K-tile's issue is then one
-// m0 write + one buffer_load per piece instead of 64-bit address math and exec-masked range
-// selects per piece. Out-of-range rows get kOOBp, which stays past num_records with any K
-// advance added. Layout 1 needs no K-range check (rows k >= K lie past the buffer's extent,
-// (K-1)*ld + idx_max, as ld >= idx_max); layout 0 needs full K-tiles (gk < K), so the caller
-// uses it only when K % 64 == 0 for every layout-0 operand.
-constexpr unsigned kOOBp = 0x80000000u;
-
-// pieces per loader wave (ROWS / 8 of them over NW waves; 288 rows over 8 waves: 5 or 4)
-template <int ROWS, int NW>
-constexpr int dma_per() { return (ROWS / 8 + NW - 1) / NW; }
-
-template <int LAYOUT, int ROWS, int NW>
-DEV void dma_prep(int64_t ld, int64_t idx0, int64_t idx_max, int wave, int lane, unsigned (&vo)[dma_per<ROWS, NW>()]) {
-#pragma unroll
-  for (int i = 0; i < dma_per<ROWS, NW>(); ++i) {
-    const int pc = wave + NW * i;
-    int64_t gi, rel;
-    if (LAYOUT == 0) {
-      const int row = pc * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      gi = idx0 + row;
-      rel = gi * ld + chunk * 8;
-    } else {
-      constexpr int RB = ROWS * 2;
-      const int byte = pc * 1024 + lane * 16;
-      const int k = byte / RB, b = byte % RB;
-      const int unit = upos<ROWS>(b >> 5, k), half = (b >> 4) & 1;
-      gi = idx0 + unit * 16 + half * 8;
-      rel = k * ld + gi;
-    }
-    vo[i] = gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
-  }
-}
-
-template <int ROWS, int NW>
-DEV void dma_issue(__amdgpu_buffer_rsrc_t rsrc, const unsigned* vo, int soff, char* lds, int wave) {
-#pragma unroll
-  for (int i = 0; i < dma_per<ROWS, NW>(); ++i) {
-    if ((ROWS / 8) % NW != 0 && wave + NW * i >= ROWS / 8) break;  // wave-uniform
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (wave + NW * i) * 1024), 16, vo[i], soff, 0, 0);
-  }
-}
-
-// L2 prefetch of K-tile kt + 2 (round 3). The 2-stage loop gives each K-tile's LDS-DMA one
-// tile of MFMAs (~2,000 cycles) to land, and the dW / forward panels mostly miss the 4 MB L2
-// (PMC: ~4x the algorithmic bytes come from the Infinity Cache / HBM), so misses sit in the
-// per-tile vmcnt(0). One extra 4-byte-per-lane LDS-DMA per wave touches every 128-B line of
-// the tile two K-steps ahead (A lines on waves 0-3, B lines on waves 4-7; a line per lane),
-// pulling it into L2 a tile early; its data lands in a dummy LDS slot nobody reads, so it
-// needs no register and no ordering, only a counted wait (vmcnt(1) instead of 0: it is the
-// wave's youngest memory operation). Out-of-range rows get kOOBp (dropped by the range check).
-// Lines of a layout-0 operand: one per row (64 k = 128 B); of a layout-1 operand: ROWS*2/128
-// per k-row.
-template <int LAYOUT, int ROWS>
-DEV unsigned pf_prep(int64_t ld, int64_t idx0, int64_t idx_max, int li) {
-  int64_t gi, rel;
-  if (LAYOUT == 0) {
-    gi = idx0 + li;
-    rel = gi * ld;
-  } else {
-    constexpr int LPR = ROWS * 2 / 128;  // lines per k-row
-    const int k = li / LPR, ch = li % LPR;
-    gi = idx0 + ch * 64;
-    rel = (int64_t)k * ld + gi;
-  }
-  return gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
-}
-
-// scalar byte offset of K-tile origin k0 for an operand of layout L
-template <int L>
-DEV int dma_soff(int64_t k0, int64_t ld) { return (int)(L == 0 ? k0 * 2 : k0 * ld * 2); }
-
-template <int ROWS>
-DEV int img1w_off(int k, int unit) { return k * (ROWS * 2) + (upos<ROWS>(unit, k) << 5); }
-
-// Transposed fragment reads issued by inline asm. The ds_read_tr16 builtin carries no
-// memory-operand info, so hipcc (ROCm 7.2) assumes it may alias the in-flight LDS-DMA of the
-// next stage and waits vmcnt(0) before it, serialising the prefetch (measured: the (0,1)
-// and (1,1) kernels lost 25-45 % to it). The asm reads are invisible to the compiler's
-// counters: tr_issue() only issues, tr_wait() (ONE s_waitcnt lgkmcnt(0) that ties the
-// destination registers) must run before any consumer (cdna_hip_programming.md §5.7 item 1,
-// form (ii) + rule 18's sched_barrier). Older compiler-issued LDS reads are also retired by
-// that wait, and extra younger asm reads only make the compiler's own counted waits stricter.
-DEV unsigned lds_addr(const char* p) {
-  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
-}
-
-template <int ROWS>
-DEV void tr_issue(const char* lds, int rbase, int ks, int lane, s16x4& lo, s16x4& hi) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int unit = rbase >> 4;
-  const int k1 = ks * 32 + 8 * g + q;
-  const unsigned a0 = lds_addr(lds + img1w_off<ROWS>(k1, unit) + 8 * p);
-  const unsigned a1 = lds_addr(lds + img1w_off<ROWS>(k1 + 4, unit) + 8 * p);
-  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
-               : "=&v"(lo), "=&v"(hi)
-               : "v"(a0), "v"(a1)
-               : "memory");
-}
-
-DEV frag8 tr_join(const s16x4& lo, const s16x4& hi) {
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(frag8, v);
-}
-
-// wait for every outstanding LDS read and tie up to 4 fragment pairs (rule 18 fence after)
-DEV void tr_wait4(s16x4& a, s16x4& b, s16x4& c, s16x4& d, s16x4& e, s16x4& f, s16x4& g, s16x4& h) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
-               :: "memory");
-}
-
-template <int N>
-DEV void tie_all(s16x4 (&lo)[N], s16x4 (&hi)[N]) {
-  s16x4 d0 = {}, d1 = {}, d2 = {}, d3 = {}, d4 = {}, d5 = {};
-#pragma unroll
-  for (int i = 0; i < N; i += 4) {
-    if (i + 3 < N) tr_wait4(lo[i], hi[i], lo[i + 1], hi[i + 1], lo[i + 2], hi[i + 2], lo[i + 3], hi[i + 3]);
-    else if (i + 1 < N) tr_wait4(lo[i], hi[i], lo[i + 1], hi[i + 1], d0, d1, d2, d3);
-    else tr_wait4(lo[i], hi[i], d0, d1, d2, d3, d4, d5);
-  }
-}
-
-// fragment X[idx = rbase + (lane&15)][k = ks*32 + 8*(lane>>4) + j] from a ROWS-wide image
-template <int LAYOUT, int ROWS>
-DEV frag8 read_frag_w(const char* lds, int rbase, int ks, int lane) {
-  if (LAYOUT == 0) return read_frag<0>(lds, rbase, ks, lane);
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int unit = rbase >> 4;
-  const int k1 = ks * 32 + 8 * g + q;
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1w_off<ROWS>(k1, unit) + 8 * p));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img1w_off<ROWS>(k1 + 4, unit) + 8 * p));
-  typedef __attribute__((ext_vector_type(8))) short s16x8;
-  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(frag8, v);
-}
-
-// one K-tile of MFMAs from the LDS stage at cur (both 32-wide K halves)
-template <int AL, int BL, int BM2, int BN, int TMW, int TN>
-DEV void tile_mfma(const char* cur_c, int wm, int wn, int lane, f32x4 (&acc)[TMW][TN]) {
-  constexpr int TILE_A = BM2 * BK * 2;
-  constexpr int WN_COLS = BN / 4;
-  char* cur = const_cast<char*>(cur_c);
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    frag8 fb[TN];
-    s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
-    if constexpr (BL == 1) {
-#pragma unroll
-      for (int t = 0; t < TN; ++t) tr_issue<BN>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane, blo[t], bhi[t]);
-    }
-    if constexpr (AL == 1) {
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * (BM2 / 2) + tm * 16, ks, lane, alo[tm], ahi[tm]);
-    }
-    if constexpr (BL == 1) tie_all<TN>(blo, bhi);
-    if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
-    if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int t = 0; t < TN; ++t)
-      fb[t] = BL == 1 ? tr_join(blo[t], bhi[t]) : read_frag<0>(cur + TILE_A, wn * WN_COLS + t * 16, ks, lane);
-#pragma unroll
-    for (int tm = 0; tm < TMW; ++tm) {
-      const frag8 fa = AL == 1 ? tr_join(alo[tm], ahi[tm]) : read_frag<0>(cur, wm * (BM2 / 2) + tm * 16, ks, lane);
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
-    }
-  }
-}
-
-// LDR selects which waves stage the next K-tile: 0 = all eight (each wave issues its share of
-// LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
-// 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
-// partner wave's MFMAs instead of beside nothing).
-// One tile's K-tiles [kb, ke) into acc (zeroed here): LDS-DMA double buffer, one barrier per
-// K-tile, the MFMA loop of the 8-wave kernels (shared by the data-parallel and stream-K kernels)
-template <int AL, int BL, int BM2, int BN, int LDR, int TMW, int TN>
-DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int64_t m0,
-                      int64_t n0, int kb, int ke, char* smem, int wave, int lane, f32x4 (&acc)[TMW][TN]) {
-  constexpr int TILE_A = BM2 * BK * 2;
-  constexpr int TILE_B = BN * BK * 2;
-  constexpr int STAGE = TILE_A + TILE_B;
-  const int wm = wave >> 2, wn = wave & 3;
-#pragma unroll
-  for (int i = 0; i < TMW; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, (int64_t)kb * BK, p.K, smem, wave, lane);
-  dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, (int64_t)kb * BK, p.K, smem + TILE_A, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  if (p.dma_pre) {
-    constexpr int NWL = LDR == 0 ? 8 : 4;
-    const int lw = LDR == 0 ? wave : (wave & 3);
-    const bool loader = LDR == 0 || (LDR == 1 ? wave < 4 : wave >= 4);
-    unsigned va[dma_per<BM2, NWL>()], vb[dma_per<BN, NWL>()];
-    dma_prep<AL, BM2, NWL>(p.lda, m0, p.M, lw, lane, va);
-    dma_prep<BL, BN, NWL>(p.ldb, n0, p.N, lw, lane, vb);
-    // prefetch lanes: waves 0-3 the first 256 A lines, waves 4-7 the B lines
-    const bool pf_a = wave < 4;
-    const unsigned vpf = pf_a ? pf_prep<AL, BM2>(p.lda, m0, p.M, wave * 64 + lane)
-                              : pf_prep<BL, BN>(p.ldb, n0, p.N, (wave - 4) * 64 + lane);
-    char* pf_slot = smem + p.pf_lds;
-    for (int kt = kb; kt < ke; ++kt) {
-      char* cur = smem + ((kt - kb) & 1) * STAGE;
-      char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
-      const int64_t k1 = (int64_t)(kt + 1) * BK;
-      if (kt + 1 < ke && loader) {
-        dma_issue<BM2, NWL>(ra, va, dma_soff<AL>(k1, p.lda), nxt, lw);
-        dma_issue<BN, NWL>(rb, vb, dma_soff<BL>(k1, p.ldb), nxt + TILE_A, lw);
-      }
-      const bool pf = p.pf && kt + 2 < ke;  // uniform
-      if (pf) {
-        const int64_t k2 = (int64_t)(kt + 2) * BK;
-        if (pf_a) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)pf_slot, 4, vpf, dma_soff<AL>(k2, p.lda), 0, 0);
-        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)pf_slot, 4, vpf, dma_soff<BL>(k2, p.ldb), 0, 0);
-      }
-      tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
-      // every DMA of tile kt+1 landed; the prefetch (this wave's youngest operation) may fly on.
-      // A raw s_barrier: __syncthreads()'s fence would add vmcnt(0) and wait for the prefetch.
-      if (pf) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-
-  for (int kt = kb; kt < ke; ++kt) {
-    char* cur = smem + ((kt - kb) & 1) * STAGE;
-    const bool more = kt + 1 < ke;
-    char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
-    const int64_t k1 = (int64_t)(kt + 1) * BK;
-    // next K-tile's LDS-DMA pieces, all issued before this tile's MFMAs (issuing them one by
-    // one between MFMA groups measured 5-15 % slower, profiles/r01/gemm_8phase.md)
-    if (more) {
-      if constexpr (LDR == 0) {
-        dma_tile<AL, BM2, 8>(ra, p.lda, m0, p.M, k1, p.K, nxt, wave, lane);
-        dma_tile<BL, BN, 8>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, wave, lane);
-      } else {
-        const bool loader = LDR == 1 ? wave < 4 : wave >= 4;
-        if (loader) {
-          const int lw = wave & 3;
-          dma_tile<AL, BM2, 4>(ra, p.lda, m0, p.M, k1, p.K, nxt, lw, lane);
-          dma_tile<BL, BN, 4>(rb, p.ldb, n0, p.N, k1, p.K, nxt + TILE_A, lw, lane);
-        }
-      }
-    }
-    tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-}
-
-// grouped, XCD-friendly tile order: virtual tile index -> (m0, n0)
-template <int BM2, int BN>
-DEV void tile_origin(const GemmArgs& p, int lid, int64_t& m0, int64_t& n0) {
-  if (p.group_m < 0) {
-    const int gn = -p.group_m;
-    const int per_group = gn * p.tiles_m;
-    const int group = lid / per_group;
-    const int first_n = group * gn;
-    const int gsize = min(p.tiles_n - first_n, gn);
-    n0 = (int64_t)(first_n + (lid % per_group) % gsize) * BN;
-    m0 = (int64_t)((lid % per_group) / gsize) * BM2;
-    return;
-  }
-  const int gm = p.group_m;
-  const int per_group = gm * p.tiles_n;
-  const int group = lid / per_group;
-  const int first_m = group * gm;
-  const int gsize = min(p.tiles_m - first_m, gm);
-  m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
-  n0 = (int64_t)((lid % per_group) / gsize) * BN;
 }
 
 // LDR selects which waves stage the next K-tile: 0 = all eight (each wave issues its share of
@@ -1011,59 +274,6 @@ __global__ __launch_bounds__(512) void gemm_sk_fixup_k(GemmArgs p) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4);
   }
-}
-
-// ============================================================================================
-// 256x256 tile, BK = 32, 4 LDS stages: LDS-DMA kept two K-tiles ahead across raw barriers
-// ============================================================================================
-// The 2-stage kernel above drains vmcnt(0) + a full barrier every K-tile, so each tile's DMA
-// has one tile of MFMAs (~1,000 cycles per SIMD) to land: L2 misses are exposed
-// (cdna_hip_programming.md "Pipelining across barriers": 3-buffer span beats 2-buffer overlap
-// at ~1 block/CU). Here a stage is a 32-deep K-tile (A 16 KiB + B 16 KiB), four stages fill
-// 128 KiB, tile kt+3 is issued while tile kt is computed, and the wait before each raw
-// s_barrier only retires tile kt+1 (vmcnt(8): tiles kt+2, kt+3 stay in flight).
-//   RAW: tile kt+1 is waited for before the barrier that ends iteration kt and read after it.
-//   WAR: slot (kt+3)%4 held tile kt-1, whose fragments were all read (and consumed by MFMAs)
-//        before the barrier that ended iteration kt-1, which precedes this issue.
-// Layout-0 images are [rows][32 k] with 64-B rows: 16-B chunk c of row r sits at slot
-// c ^ ((r >> 2) & 2), which makes every ds_read_b128 lane group of 16 hit 16 distinct bank slots
-// (rows r..r+15 of one fragment, chunks 0/1 or 2/3 per group). Layout-1 images are [32 k][rows]
-// read with ds_read_b64_tr_b16, as in the 64-deep kernels.
-constexpr int BK32 = 32;
-
-DEV int img0h_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 2)) << 4); }
-
-// one [ROWS][32] (layout 0) or [32][ROWS] (layout 1) operand image, 8 waves
-template <int LAYOUT, int ROWS>
-DEV void dma_tile32(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
-                    char* lds, int wave, int lane) {
-  constexpr int kPieces = ROWS / 16;  // 1 KiB pieces: 16 rows of 64 B, or 2 k-rows of ROWS*2 B (ROWS = 256)
-#pragma unroll
-  for (int i = 0; i < kPieces / 8; ++i) {
-    const int pc = wave + 8 * i;
-    unsigned off;
-    if (LAYOUT == 0) {
-      const int row = pc * 16 + (lane >> 2);
-      const int chunk = (lane & 3) ^ ((row >> 2) & 2);
-      const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
-      off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
-    } else {
-      constexpr int RB = ROWS * 2;
-      const int byte = pc * 1024 + lane * 16;
-      const int k = byte / RB, b = byte % RB;
-      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
-      const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
-      off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
-  }
-}
-
-// retire all but n (wave-uniform, in K-tiles of 4 DMA instructions) of this wave's tiles
-DEV void wait_tiles4(int n) {
-  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int AL, int BL, int CT>
@@ -1651,7 +861,8 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
 // is roughly fixed, so a taller tile amortises it over more MFMAs, and M = 8704 = 30.2 x 288
 // makes the N = 4096 products (every dX, o and down forward) 496 tiles = 1.94 rounds instead of
 // 736 192-row tiles = 2.88 rounds.
-enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8, kT288x256 = 10 };
+enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8, kT288x256 = 10,
+       kTpp4 = 12, kTpp5 = 13 };
 // plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
 double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
@@ -1716,7 +927,8 @@ extern "C" int cullavo_gemm_set_streamk(int mode) {
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11) ? mode : -1;
+  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11 || mode == kTpp4 || mode == kTpp5) ? mode
+                                                                                                        : -1;
   return prev;
 }
 
@@ -1768,8 +980,8 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
   if ((tile == 7 || tile == 11) && a_layout != 0) tile = 6;
-  static const int bm[12] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288};
-  static const int bn[12] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  static const int bm[14] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288, 256, 256};
+  static const int bn[14] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -1874,6 +1086,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     L8P(1, 1)
 #undef L8P
   }
+  if (tile == kTpp4 || tile == kTpp5) return cvgemm_launch_pp(p, tile == kTpp4 ? 4 : 5, a_layout, b_layout, f32, s);
   if (tile == kT4s) {
 #define L4S(AL, BL) return f32 ? launch4s<AL, BL, CULLAVO_DT_F32>(p, s) : launch4s<AL, BL, CULLAVO_DT_BF16>(p, s);
     if (a_layout == 0 && b_layout == 0) { L4S(0, 0) }

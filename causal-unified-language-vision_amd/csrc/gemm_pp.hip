@@ -1,0 +1,247 @@
+// 256x256 wave-group ping-pong GEMM (tile modes 12 / 13), its own translation unit so the kernel
+// compiles apart from the other GEMM families (gemm.hip dispatches to cvgemm_launch_pp).
+#include "gemm_common.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+using namespace cvgemm;
+
+// ============================================================================================
+// 256x256 wave-group ping-pong (round 4, tile modes 12 / 13): 32-deep K-tiles in NS LDS slots
+// ============================================================================================
+// The 2-stage loop (gemm256_k) ends every 64-deep K-tile with vmcnt(0) + a workgroup barrier, so
+// both waves of a SIMD run their LDS-DMA issue, fragment reads and MFMAs in the same phase: the
+// DMA issue (~60-185 cycles per 1 KiB piece, MI355X_MICROARCH.md cycle constants) sits in front
+// of both waves' MFMAs and the matrix pipe idles (MFMA busy 0.52 on the dW family). Here the two
+// waves of each SIMD take turns (MI355X_MICROARCH.md §Two waves per SIMD items 1 and 9):
+//   phase 2t   : waves 0-3 LOAD tile t   | waves 4-7 COMPUTE tile t-1
+//   phase 2t+1 : waves 0-3 COMPUTE tile t | waves 4-7 LOAD tile t
+// with one workgroup barrier per phase. A LOAD segment issues the wave's 4 LDS-DMA pieces of tile
+// t+NS-1 (A pieces w, w+8 and B pieces w, w+8 of the 16 + 16 per tile) and reads its 12 fragments
+// of tile t (8 A rows-of-16 x 32 k, 4 B) into registers; a COMPUTE segment is 32 MFMAs on
+// registers only (no LDS access, no VALU), so one wave's memory work runs under its partner's
+// matrix work. Waves 4-7 start one barrier late and waves 0-3 end with one extra barrier.
+//   RAW: in LOAD(t) each wave waits (counted vmcnt) for its own pieces of tile t+1 before the
+//        barrier ending that phase; tile t+1 is first read in phase 2t+2, after both groups'
+//        waits and a barrier.
+//   WAR: slot (t+NS-1) % NS held tile t-1, last read in phase 2t-1 (waves 4-7's LOAD(t-1)); the
+//        earliest refill is waves 0-3's LOAD(t) in phase 2t.
+// Each tile's buffer descriptor is rebased to the tile's K origin (num_records shrunk by the
+// same bytes) and the per-lane offsets are tile-relative, so rows past K (layout 1) fall outside
+// num_records and read as zeros without relying on the scalar offset being range-checked; a
+// layout-0 operand's K tail (K % 32 != 0) takes a per-lane column check on the last tile.
+constexpr int kPPStage = 2 * 256 * BK32 * 2;  // A + B image of one 32-deep tile: 32 KiB
+
+// retire all but n (wave-uniform, 0..3) of this wave's 4-piece tiles
+DEV void pp_wait(int n) {
+  if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// per-lane source offset (elements x 2, tile-relative) of piece pc of a [256][32] (layout 0) or
+// [32][256] (layout 1) image; kcheck >= 0: zero-fill columns k0 + c >= K (layout 0 tail tile)
+template <int LAYOUT>
+DEV unsigned pp_voff(int64_t ld, int64_t idx0, int64_t idx_max, int pc, int lane, int64_t kleft) {
+  int64_t gi, rel;
+  if (LAYOUT == 0) {
+    const int row = pc * 16 + (lane >> 2);
+    const int chunk = (lane & 3) ^ ((row >> 2) & 2);
+    gi = idx0 + row;
+    rel = gi * ld + chunk * 8;
+    if (chunk * 8 >= kleft) return kOOBp;
+  } else {
+    const int byte = pc * 1024 + lane * 16;
+    const int k = byte >> 9, b = byte & 511;
+    const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
+    gi = idx0 + unit * 16 + half * 8;
+    rel = (int64_t)k * ld + gi;
+  }
+  return gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
+}
+
+// descriptor of operand X rebased to K origin k0 (bytes = the operand's full extent)
+template <int LAYOUT>
+DEV __amdgpu_buffer_rsrc_t pp_rsrc(const u16* X, int64_t ld, int64_t bytes, int64_t k0) {
+  const int64_t off = (LAYOUT == 0 ? k0 : k0 * ld) * 2;
+  const int64_t left = bytes - off;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)X + off), (short)0, (int)(left > 0 ? left : 0),
+                                           0x00020000);
+}
+
+// this wave's 4 LDS-DMA pieces of tile t into its slot
+template <int AL, int BL, int NS>
+DEV void pp_issue(const GemmArgs& p, int64_t a_bytes, int64_t b_bytes, const unsigned (&va)[2],
+                  const unsigned (&vb)[2], int64_t m0, int64_t n0, int t, int nk, int64_t ktail, char* smem,
+                  int wave, int lane) {
+  constexpr int TILE_A = 256 * BK32 * 2;
+  char* dst = smem + (t % NS) * kPPStage;
+  const int64_t k0 = (int64_t)t * BK32;
+  const __amdgpu_buffer_rsrc_t ra = pp_rsrc<AL>(p.A, p.lda, a_bytes, k0);
+  const __amdgpu_buffer_rsrc_t rb = pp_rsrc<BL>(p.B, p.ldb, b_bytes, k0);
+  unsigned a0 = va[0], a1 = va[1], b0 = vb[0], b1 = vb[1];
+  if ((AL == 0 || BL == 0) && t == nk - 1 && ktail < BK32) {  // wave-uniform
+    if (AL == 0) {
+      a0 = pp_voff<0>(p.lda, m0, p.M, wave, lane, ktail);
+      a1 = pp_voff<0>(p.lda, m0, p.M, wave + 8, lane, ktail);
+    }
+    if (BL == 0) {
+      b0 = pp_voff<0>(p.ldb, n0, p.N, wave, lane, ktail);
+      b1 = pp_voff<0>(p.ldb, n0, p.N, wave + 8, lane, ktail);
+    }
+  }
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(dst + wave * 1024), 16, a0, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(dst + (wave + 8) * 1024), 16, a1, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + TILE_A + wave * 1024), 16, b0, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + TILE_A + (wave + 8) * 1024), 16, b1, 0, 0, 0);
+}
+
+template <int AL, int BL, int CT, int NS>
+__global__ __launch_bounds__(512, 1) void gemmpp_k(GemmArgs p) {
+  static_assert(NS == 4 || NS == 5, "slot count");
+  constexpr int TILE_A = 256 * BK32 * 2;
+  constexpr int TN = 4, TMW = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lid = xcd_remap(blockIdx.x, p.tiles_m * p.tiles_n);
+  int64_t tm0, tn0;
+  tile_origin<256, 256>(p, lid, tm0, tn0);
+  const int64_t m0 = tm0, n0 = tn0;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
+  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
+  const int nk = (int)cdiv(p.K, BK32);
+  const int64_t ktail = p.K - (int64_t)(nk - 1) * BK32;  // columns of the last tile (1..32)
+
+  unsigned va[2], vb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    va[i] = pp_voff<AL>(p.lda, m0, p.M, wave + 8 * i, lane, BK32);
+    vb[i] = pp_voff<BL>(p.ldb, n0, p.N, wave + 8 * i, lane, BK32);
+  }
+  f32x4 acc[TMW][TN];
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) pp_issue<AL, BL, NS>(p, a_bytes, b_bytes, va, vb, m0, n0, t, nk, ktail, smem, wave, lane);
+  pp_wait(min(NS - 2, nk - 1));  // this wave's pieces of tile 0 landed
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // waves 4-7 run one phase behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  // lab ablations (CULLAVO_PP_ABL, host env; results are wrong with bits 0, 3, 4): 1 no
+  // steady-state DMA, 2 no vmcnt waits, 4 no explicit lgkmcnt wait, 8 fragments read once (tile
+  // 0 only), 16 no barriers in the loop, 32 DMA issued after the fragment reads, 64 no setprio
+  const int abl = p.pf;
+  frag8 fa[TMW], fb[TN];
+  for (int t = 0; t < nk; ++t) {
+    // ---- LOAD segment: DMA of tile t+NS-1, fragments of tile t ----
+    const char* cur = smem + (t % NS) * kPPStage;
+    const bool dma = t + NS - 1 < nk && !(abl & 1);
+    if (dma && !(abl & 32))
+      pp_issue<AL, BL, NS>(p, a_bytes, b_bytes, va, vb, m0, n0, t + NS - 1, nk, ktail, smem, wave, lane);
+    s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
+    if (!(abl & 8) || t == 0) {
+    if constexpr (BL == 1) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) tr_issue<256>(cur + TILE_A, wn * 64 + j * 16, 0, lane, blo[j], bhi[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * 64 + j * 16 + (lane & 15);
+        fb[j] = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + TILE_A + img0h_off(row, lane >> 4)));
+      }
+    }
+    if constexpr (AL == 1) {
+#pragma unroll
+      for (int i = 0; i < TMW; ++i) tr_issue<256>(cur, wm * 128 + i * 16, 0, lane, alo[i], ahi[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TMW; ++i) {
+        const int row = wm * 128 + i * 16 + (lane & 15);
+        fa[i] = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + img0h_off(row, lane >> 4)));
+      }
+    }
+    if constexpr (BL == 1) tie_all<TN>(blo, bhi);
+    if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      if constexpr (BL == 1) fb[j] = tr_join(blo[j], bhi[j]);
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+      if constexpr (AL == 1) fa[i] = tr_join(alo[i], ahi[i]);
+    }
+    if (dma && (abl & 32))
+      pp_issue<AL, BL, NS>(p, a_bytes, b_bytes, va, vb, m0, n0, t + NS - 1, nk, ktail, smem, wave, lane);
+    // this wave's pieces of tile t+1 landed (tiles up to t+NS-1 may stay in flight)
+    if (!(abl & 2)) pp_wait(min(t + NS - 1, nk - 1) - (t + 1));
+    if (!(abl & 4)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(abl & 16)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- COMPUTE segment: 32 MFMAs on registers ----
+    if (!(abl & 64)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(abl & 16)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // pairs with waves 4-7's last COMPUTE barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if (p.epi_lds) {
+    lds_epilogue<CT, 256, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TMW; ++i) {
+    const int64_t m = m0 + wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) store4<CT>(p, acc[i][j], m, n0 + wn * 64 + j * 16 + (lane >> 4) * 4);
+  }
+}
+
+template <int AL, int BL, int CT, int NS>
+int launchpp(GemmArgs p, hipStream_t s) {
+  const int smem = std::max(NS * kPPStage, 128 * 1024);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemmpp_k<AL, BL, CT, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_n = (int)cdiv(p.N, 256);
+  static const int abl = getenv("CULLAVO_PP_ABL") ? atoi(getenv("CULLAVO_PP_ABL")) : 0;
+  p.pf = abl;
+  gemmpp_k<AL, BL, CT, NS><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemmpp");
+}
+
+}  // namespace
+
+int cvgemm_launch_pp(const cvgemm::GemmArgs& p, int ns, int a_layout, int b_layout, bool f32, hipStream_t s) {
+#define LPP(AL, BL)                                                                                             \
+  if (ns == 4) return f32 ? launchpp<AL, BL, CULLAVO_DT_F32, 4>(p, s) : launchpp<AL, BL, CULLAVO_DT_BF16, 4>(p, s); \
+  return f32 ? launchpp<AL, BL, CULLAVO_DT_F32, 5>(p, s) : launchpp<AL, BL, CULLAVO_DT_BF16, 5>(p, s);
+  if (a_layout == 0 && b_layout == 0) { LPP(0, 0) }
+  if (a_layout == 0 && b_layout == 1) { LPP(0, 1) }
+  if (a_layout == 1 && b_layout == 0) { LPP(1, 0) }
+  LPP(1, 1)
+#undef LPP
+}
