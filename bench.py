@@ -57,9 +57,10 @@ def parse(argv=None):
                     help="run the optimizer update on a side stream under the next forward (A/B; off by default)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="optimizer update in-stream (the default; kept for A/B scripts)")
-    ap.add_argument("--workload", default="step", choices=["step", "vit"],
+    ap.add_argument("--workload", default="step", choices=["step", "vit", "decode"],
                     help="step: the training step (default; configs 3/4/5 by --config/--batch/--text-len); "
-                         "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64)")
+                         "vit: BASELINE config 2, the CLIP ViT-L/14-336 encoder forward at bs=--batch (64); "
+                         "decode: 7B KV-cache decode (the step-2-pre generate path) at batch --batch")
     ap.add_argument("--sub-workloads", default=",".join(SUB_WORKLOADS),
                     help="N=1 headline runs only: the other workloads timed in child processes ('' = none)")
     ap.add_argument("--no-sub", action="store_true", help="time this workload only")
@@ -74,6 +75,8 @@ SUB_WORKLOADS = {
     "config2-vit": ["--workload", "vit", "--batch", "64"],
     "config5-full": ["--config", "llava-1.5-13b", "--batch", "4", "--text-len", "1025"],
     "config3-lora": ["--trainable", "lora"],
+    "decode-b1": ["--workload", "decode", "--batch", "1"],
+    "decode-b8": ["--workload", "decode", "--batch", "8"],
 }
 
 
@@ -81,6 +84,8 @@ def workload_key(args) -> str:
     """the key PMC records are filed under (profiles/roofline_traffic.json)"""
     if args.workload == "vit":
         return "config2-vit"
+    if args.workload == "decode":
+        return f"decode-b{args.batch}"
     return f"{'config5' if '13b' in args.config else 'config3'}-{args.trainable}"
 
 
@@ -104,7 +109,8 @@ def run_sub_workloads(args, names):
             out[name] = {"error": "timed out after 600 s"}
             continue
         keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops_per_gpu", "mfu",
-                "gflop_per_image", "loss", "roofline", "gemm_kernels", "gemm_shapes")
+                "gflop_per_image", "loss", "roofline", "gemm_kernels", "gemm_shapes", "prefill_ms", "weight_bytes",
+                "step_roofline")
         out[name] = {k: rec[k] for k in keep if k in rec}
         out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
     return out
@@ -196,6 +202,93 @@ def vit_main(args):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def decode_main(args):
+    """KV-cache decode of the 7B LM (the step-2-pre generate() loop,
+    reference cullavo/arch_cullavo.py:365 and the cached branch :605-636): prefill of the config-3
+    prompt (336 px image + 513 text tokens -> 1088 merged rows) at batch --batch, then timed decode
+    steps replayed from the captured HIP graph (generation.DecodeGraph). value = generated tokens/s
+    over all sequences. Roofline: HBM, the weight-streaming GEMV (gemv_k) -- the bytes one launch
+    must read (W, X, C) over its mean launch time, measured with HIP events on an eager step -- and
+    the whole step's weight stream (13.2 GB of LM + head weights per token step / step time)."""
+    import torch
+
+    from cullavo_amd import ops
+    from cullavo_amd.arch_cullavo import CuLLaVOModel
+    from cullavo_amd.config import llava_1_5_7b
+    from cullavo_amd.data import synthetic_batch
+    from cullavo_amd.generation import DecodeGraph
+
+    torch.cuda.set_device(0)
+    cfg = llava_1_5_7b()
+    m = CuLLaVOModel(cfg, device="cuda", trainable="none", init="random", seed=0)
+    m.eval()
+    B = args.batch
+    sb = synthetic_batch(cfg, B, args.text_len, 35, seed=1234, device="cuda")
+    t = cfg.text_config
+    wbytes = 2 * (t.num_hidden_layers * (4 * t.hidden_size ** 2 + 3 * t.hidden_size * t.intermediate_size)
+                  + t.vocab_size * t.hidden_size)
+    n_tok = max(32, 8 * args.steps)
+    L0 = args.text_len + cfg.vision_config.num_patches - 1
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    with torch.no_grad():
+        def prefill():
+            out = m._forward_cached(sb["input_ids"], sb["pixel_values"], sb["attention_mask"], None, None, None,
+                                    cfg.vision_feature_layer, cfg.vision_feature_select_strategy, None, True,
+                                    max_len=L0 + n_tok + 8 * args.warmup + 8)
+            return out.past_key_values, out.logits[:, -1]
+        cache, logits = prefill()  # warm (allocations, first launches)
+        # eager decode steps with every GEMM launch bracketed by events: the GEMV's own rate
+        ops.trace_gemm("all")
+        tok = torch.randint(2, 32000, (B,), device="cuda", generator=gen)
+        for _ in range(4):
+            logits = m(input_ids=tok[:, None], past_key_values=cache, use_cache=True).logits[:, -1]
+        torch.cuda.synchronize()
+        launches = ops.trace_launches()
+        ops.trace_gemm(None)
+        gv = [(k, ms) for k, ms in launches if k[0] <= 16 and k[3] == 0 and k[4] == 0]
+        g_bytes = sum(2.0 * (M * K + N * K + M * N) for (M, N, K, _, _), _ in gv)
+        g_ms = sum(ms for _, ms in gv)
+        # timed: a fresh prefill, then n_tok graph replays
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cache, logits = prefill()
+        torch.cuda.synchronize()
+        prefill_ms = (time.perf_counter() - t0) * 1e3
+        graph = DecodeGraph(m, cache)
+        for _ in range(8 * args.warmup):
+            logits = graph.step(logits.argmax(-1))[:, -1]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_tok):
+            logits = graph.step(logits.argmax(-1))[:, -1]
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    step_s = elapsed / n_tok
+    n_launch = len(gv)
+    achieved = g_bytes / (g_ms * 1e-3) / 1e9
+    line = {
+        "metric": f"7B KV-cache decode tokens/sec (batch {B}, {L0}-row prompt)", "value": round(B * n_tok / elapsed, 2),
+        "unit": "tokens/s", "n_gpus": 1, "steps": n_tok, "warmup": 8 * args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded prompt + pixels, random-init weights)",
+        "config": {"workload": f"decode: ViT-L/14-336 + Vicuna-7B, prompt 336 px + {args.text_len} tokens "
+                               f"(L0={L0}), batch {B}, greedy, one HIP-graph replay per token",
+                   "model": "llava-1.5-7b", "global_batch": B, "seq_len": L0, "parallelism": "dp1"},
+        "prefill_ms": round(prefill_ms, 2), "weight_bytes": wbytes,
+        "roofline": {"kernel": f"gemv_k<1>: decode Linears Y = X W^T at M = {B}, {n_launch // 4} launches per step "
+                               f"(eager step, HIP events per launch)",
+                     "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "algorithmic_bytes": round(g_bytes / max(n_launch, 1)),
+                     "avg_ms": round(g_ms / max(n_launch, 1), 5)},
+        "step_roofline": {"what": "LM + head weight bytes per token step / replayed step time (every kernel of the "
+                                  "step, attention and norms included)",
+                          "achieved": round(wbytes / step_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                          "frac": round(wbytes / step_s / 8e12, 4)},
+    }
+    print(json.dumps(line), flush=True)
 
 
 def cpu_baseline(cfg, text_len: int, budget_s: float):
@@ -290,7 +383,8 @@ def gemm_kernel_name(M, N, K, al=0, bl=0):
     names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0>",
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",
-             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>"}
+             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
+             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1>"}
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 
@@ -462,6 +556,8 @@ def main(argv=None):
         if args.batch == 8:
             args.batch = 64  # BASELINE config 2
         return vit_main(args)
+    if args.workload == "decode":
+        return decode_main(args)
     import torch
     import torch.distributed as dist
 

@@ -272,6 +272,12 @@ class CuLLaVOModel(nn.Module):
         logits = out.logits[:, -1]
         finished = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
         new = []
+        # the decode steps replay one captured HIP graph (generation.DecodeGraph) unless asked not to
+        graph = None
+        if kw.get("decode_graph", True) and max_new_tokens > 1 and input_ids.is_cuda:
+            from .generation import DecodeGraph
+            graph = DecodeGraph(self, cache)
+        check_every = 16  # all-finished test every 16 tokens: one host sync per 16 steps, not per step
         for step in range(max_new_tokens):
             tok = sample_next(logits, do_sample=do_sample, temperature=temperature, top_k=top_k, top_p=top_p,
                               generator=generator)
@@ -279,14 +285,25 @@ class CuLLaVOModel(nn.Module):
             new.append(tok)
             if eos_token_id is not None:
                 finished |= tok == eos_token_id
-                if bool(finished.all()):
+                if (step + 1) % check_every == 0 and bool(finished.all()):
                     break
             if step + 1 == max_new_tokens:
                 break
-            out = self._forward_cached(tok[:, None], None, None, None, cache, None, cfg.vision_feature_layer,
-                                       cfg.vision_feature_select_strategy, None, True)
-            logits = out.logits[:, -1]
-        return torch.cat([input_ids, torch.stack(new, 1).to(input_ids.dtype)], 1)
+            if graph is not None:
+                logits = graph.step(tok)[:, -1]
+            else:
+                out = self._forward_cached(tok[:, None], None, None, None, cache, None, cfg.vision_feature_layer,
+                                           cfg.vision_feature_select_strategy, None, True)
+                logits = out.logits[:, -1]
+        gen = torch.stack(new, 1)
+        if eos_token_id is not None:
+            # HF stops at the first step where every row has finished; the steps run past it (at
+            # most check_every - 1) hold only padding and are dropped
+            done = torch.cumsum((gen == eos_token_id).to(torch.int64), 1) > 0
+            all_done = done.all(0)
+            if bool(all_done.any()):
+                gen = gen[:, :int(all_done.to(torch.int64).argmax()) + 1]
+        return torch.cat([input_ids, gen.to(input_ids.dtype)], 1)
 
     # -- pieces ---------------------------------------------------------------------------------
     def _image_features(self, pixel_values, layer: int, strategy: str):

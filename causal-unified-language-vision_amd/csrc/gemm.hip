@@ -19,6 +19,8 @@
 
 // the ping-pong kernel (tile modes 12 / 13) lives in gemm_pp.hip (its own translation unit)
 int cvgemm_launch_pp(const cvgemm::GemmArgs& p, int ns, int a_layout, int b_layout, bool f32, hipStream_t s);
+// the decode-step weight-streaming product (M <= 16, forward layouts) lives in gemv.hip
+int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s);
 
 namespace {
 using namespace cvgemm;
@@ -894,6 +896,10 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 }  // namespace
 
 static int g_force_tile = -1;
+static int g_gemv = 1;  // cullavo_gemm_set_tile(0..13) forces a tiled kernel for decode rows too
+static bool gemv_eligible(int64_t M, int a_layout, int b_layout, bool dropping) {
+  return g_gemv && g_force_tile < 0 && M >= 1 && M <= 16 && a_layout == 0 && b_layout == 0 && !dropping;
+}
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
 static int g_dma_pre = 1;  // +2.7 % on the 7B step (profiles/r03/dma_ab.md)
@@ -969,6 +975,10 @@ extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
 }
 
 extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid) {
+  if (gemv_eligible(M, a_layout, b_layout, false)) {  // 14: the decode GEMV (gemv.hip)
+    if (grid) *grid = cdiv(N, 16);
+    return 14;
+  }
   if (g_force_tile < 0) {  // 9: the 8-wave 256x256 kernel split over K (given its workspace)
     int per = 0;
     const int s = splitk256_plan(M, N, K, &per);
@@ -1054,6 +1064,8 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
   const int64_t b_ext = b_layout == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N;
   const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
+  // decode rows (M = batch <= 16, Y = X W^T): stream W once through the GEMV kernel (gemv.hip)
+  if (gemv_eligible(M, a_layout, b_layout, dropping)) return cvgemm_launch_gemv(p, f32, s);
   bool split256 = false;
   {
     int per = 0, per256 = 0;

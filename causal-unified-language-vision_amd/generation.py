@@ -105,9 +105,11 @@ class KVCache:
         return cache
 
 
-def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int, start, kv_len):
+def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int, start, kv_len,
+                attn_len: int | None = None):
     """One LlamaDecoderLayer over Lnew new rows per sequence (prefill: Lnew = prompt length on an
-    empty cache; decode: Lnew = 1), appending their keys/values to the cache. No autograd."""
+    empty cache; decode: Lnew = 1), appending their keys/values to the cache. No autograd.
+    attn_len: the key range decode attention is sized for (default: the filled rows + 1)."""
     cfg = layer.cfg
     d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
     lg = layer.lora_groups
@@ -122,7 +124,8 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
         o, _ = ops.attn_fwd(q, k, v, B=B, H=H, Lq=Lnew, Lk=Lnew, D=D, scale=D ** -0.5, causal=True,
                             kv_start=sctx.kv_start)
     else:
-        o = ops.attn_decode(q, cache.k[li], cache.v[li], kv_len, B=B, H=H, D=D, max_len=cache.length + 1,
+        o = ops.attn_decode(q, cache.k[li], cache.v[li], kv_len, B=B, H=H, D=D,
+                            max_len=attn_len if attn_len is not None else cache.length + 1,
                             scale=D ** -0.5, kv_start=sctx.kv_start)
     t, _ = lg["o"].forward(o, False, 0)
     h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h, addend=t)
@@ -132,6 +135,68 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     a = ops.swiglu_fwd(gu)
     t, _ = lg["down"].forward(a, False, 0)
     return ops.linear(a, layer.mlp.down_proj.weight, residual=h2, addend=t)
+
+
+class DecodeGraph:
+    """One cached decode step of the LM -- the new token's embedding row, every decoder layer at one
+    row per sequence, the final norm and lm_head -- captured once as a HIP graph and replayed per
+    token (about 330 kernel launches per 7B step; replayed, the host no longer issues them one by
+    one). Everything the step reads that changes from token to token lives in device buffers the
+    graph owns and advances itself: the token ids (written by the caller before each replay), the
+    RoPE positions and the cache write row (+1 at the end of every replay); decode attention runs
+    over the cache's full capacity (chunks past a row's length exit at once), so the grid does not
+    depend on the current length. The cache must not grow while the graph is alive (generate()
+    sizes it for prompt + max_new_tokens)."""
+
+    def __init__(self, model, cache: KVCache):
+        lm = model.language_model
+        self.cache, self.lm = cache, lm
+        B = cache.B
+        dev = cache.k.device
+        self.ids = torch.zeros(B, dtype=torch.long, device=dev)
+        self.pos = cache.next_pos.to(torch.int64).clone()
+        self.start = torch.full((B,), cache.length, dtype=torch.int32, device=dev)
+        self.embed = model.get_input_embeddings()
+        self.graph = torch.cuda.CUDAGraph()
+        self.steps_left = cache.max_len - cache.length
+        stream = torch.cuda.Stream(device=dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        traced = ops._TRACE["key"]
+        ops._TRACE["key"] = None  # no per-launch timing events inside the captured graph
+        try:
+            with torch.cuda.stream(stream):
+                with torch.cuda.graph(self.graph, stream=stream, capture_error_mode="thread_local"):
+                    self.logits = self._step()
+        finally:
+            ops._TRACE["key"] = traced
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        cache.next_pos = self.pos  # advanced in place by every replay
+
+    def _step(self):
+        lm, cache = self.lm, self.cache
+        cfg = lm.cfg
+        B = cache.B
+        h = self.embed(self.ids[:, None]).reshape(B, cfg.hidden_size)
+        sctx = StepContext(B, 1, self.pos[:, None], cache.kv_start, lora_seed=0)
+        kv_len = self.start + 1
+        for li, layer in enumerate(lm.model.layers):
+            h = layer_infer(layer, h, sctx, cache, li, 1, self.start, kv_len, attn_len=cache.max_len)
+        x, _ = ops.rmsnorm_fwd(h, lm.model.norm.weight, cfg.rms_norm_eps)
+        logits = ops.linear(x, lm.lm_head.weight)
+        self.pos.add_(1)
+        self.start.add_(1)
+        return logits.view(B, 1, -1)
+
+    def step(self, tokens):
+        """Append `tokens` ([B] ids) to the cache and return the next logits [B, 1, V] (a view of
+        the graph's output buffer, overwritten by the next replay)."""
+        if self.steps_left <= 0:
+            raise ValueError("decode graph: the KV cache is full")
+        self.ids.copy_(tokens.reshape(-1))
+        self.graph.replay()
+        self.cache.length += 1
+        self.steps_left -= 1
+        return self.logits
 
 
 def lm_infer(lm, embeds, attention_mask, position_ids, cache: KVCache | None, max_len: int):

@@ -92,17 +92,12 @@ def trace_launches():
     return [(k, a.elapsed_time(b)) for a, b, k in evs]
 
 
-_SPLIT256 = {}
-
-
 def _split256(M, N, K, a_layout, b_layout) -> bool:
     """the library runs this problem split over K on the 8-wave kernel (cullavo_gemm_plan tile 9:
-    a small 256x256 grid with a long K), given a workspace from the caller"""
-    key = (M, N, K, a_layout, b_layout)
-    v = _SPLIT256.get(key)
-    if v is None:
-        v = _SPLIT256[key] = lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None) == 9
-    return v
+    a small 256x256 grid with a long K), given a workspace from the caller. Asked per call, not
+    cached: the plan depends on the library's forced tile and tile rates (cullavo_gemm_set_tile /
+    _set_tile_rate), which callers may change at any time (one ~1 us host call per GEMM)."""
+    return lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None) == 9
 
 
 def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,

@@ -187,3 +187,107 @@ def test_transformers_layout_cache_decode_matches_kvcache():
     assert first.shape == (2, cfg.text.num_attention_heads, native.get_seq_length())
     with pytest.raises(TypeError, match="legacy cache"):
         m(input_ids=tok, past_key_values=torch.zeros(3), attention_mask=step_mask, use_cache=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# decode-step GEMV (gemv.hip) and the captured decode graph (generation.DecodeGraph)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (8, 12288, 4096), (3, 776, 1000), (16, 4096, 11008),
+                                   (8, 32064, 4096), (5, 264, 64)])
+@pytest.mark.parametrize("epi", ["none", "residual", "addend_bias"])
+def test_gemv_decode_rows_match_fp32(M, N, K, epi):
+    """Y = X W^T for M = batch <= 16 rows goes through the weight-streaming kernel (plan tile 14)
+    with the full GEMM epilogue; checked against fp32 on the same bf16 inputs (max|err| <= 8e-3 x
+    scale, the GEMM tests' bar) and against the tiled kernel (forced tile 2: same products, other
+    f32 summation order)."""
+    from cullavo_amd import _lib, ops
+    L = _lib.lib()
+    assert L.cullavo_gemm_plan(M, N, K, 0, 0, None) == 14
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    X = torch.randn(M, K, generator=g).to(BF)
+    W = (torch.randn(N, K, generator=g) * K ** -0.5).to(BF)
+    bias = torch.randn(N, generator=g).to(BF) if epi == "addend_bias" else None
+    add = torch.randn(M, N, generator=g).to(BF) if epi == "addend_bias" else None
+    res = torch.randn(M, N, generator=g).to(BF) if epi == "residual" else None
+    z = X.float() @ W.float().T
+    if bias is not None:
+        z = (z + bias.float()).to(BF).float() + add.float()
+    if res is not None:
+        z = z.to(BF).float() + res.float()
+    dev = lambda t: t.cuda() if t is not None else None
+    outs = []
+    for tile in (-1, 2):
+        prev = L.cullavo_gemm_set_tile(tile)
+        try:
+            C = torch.empty(M, N, dtype=BF, device="cuda")
+            ops.gemm_ex(0, 0, M, N, K, dev(X), K, dev(W), K, C, N, bias=dev(bias), addend=dev(add),
+                        ld_addend=N if add is not None else 0, residual=dev(res), ldr=N if res is not None else 0)
+            torch.cuda.synchronize()
+        finally:
+            L.cullavo_gemm_set_tile(prev)
+        outs.append(C.float().cpu())
+    for o in outs:
+        assert (o - z).abs().max().item() <= 8e-3 * z.abs().max().item()
+    assert rel_l2(outs[0], outs[1]) <= 4e-3
+
+
+@pytest.mark.gpu
+def test_decode_graph_matches_eager_steps():
+    """The captured decode step (HIP graph replay, attention sized for the cache capacity) gives
+    bitwise the logits of the eager cached forward, step after step, and advances the cache the
+    same way; generate() with and without the graph returns the same tokens."""
+    from cullavo_amd.generation import DecodeGraph, KVCache
+    cfg = O.config_small_gpu()
+    m = _model(6)
+    ids, mask, pix, _ = O.make_inputs(cfg, 2, 20, 3, 21)
+    ids, mask, pix = ids.cuda(), mask.cuda(), pix.cuda()
+    L0 = 20 + cfg.vision.num_patches - 1
+    runs = []
+    for use_graph in (False, True):
+        out = m._forward_cached(ids, pix, mask, None, None, None, -2, "default", None, True, max_len=L0 + 8)
+        cache = out.past_key_values
+        graph = DecodeGraph(m, cache) if use_graph else None
+        toks = torch.randint(2, cfg.image_token_index, (6, 2), generator=torch.Generator().manual_seed(9)).cuda()
+        steps = []
+        for i in range(6):
+            if graph is not None:
+                lg = graph.step(toks[i]).clone()
+            else:
+                lg = m(input_ids=toks[i][:, None], past_key_values=cache, use_cache=True).logits.clone()
+            steps.append(lg)
+        runs.append((steps, cache))
+    for i, (a, b) in enumerate(zip(runs[0][0], runs[1][0])):
+        assert torch.equal(a, b), i
+    ca, cb = runs[0][1], runs[1][1]
+    assert ca.length == cb.length == L0 + 6
+    assert torch.equal(ca.k[:, :, :ca.length], cb.k[:, :, :cb.length])
+    assert torch.equal(ca.next_pos, cb.next_pos)
+    kw = dict(input_ids=ids, pixel_values=pix, attention_mask=mask, max_new_tokens=7)
+    assert torch.equal(m.generate(**kw), m.generate(**kw, decode_graph=False))
+
+
+@pytest.mark.gpu
+def test_generate_eos_stop_with_sparse_checks():
+    """generate() tests 'all rows finished' every 16 tokens and trims the padding-only steps it ran
+    past the stop: the result equals the per-step-checked loop (an eos that every row emits)."""
+    cfg = O.config_small_gpu()
+    m = _model(6)
+    ids, mask, pix, _ = O.make_inputs(cfg, 2, 20, 3, 23)
+    kw = dict(input_ids=ids.cuda(), pixel_values=pix.cuda(), attention_mask=mask.cuda(), max_new_tokens=40)
+    free = m.generate(**kw)
+    eos = int(free[0, 23])  # row 0's 4th new token: row 1 may finish later or never (then no stop)
+    out = m.generate(**kw, eos_token_id=eos)
+    gen = out[:, 20:].cpu()
+    fin = torch.cumsum((gen == eos).long(), 1) > 0
+    all_done = fin.all(0)
+    if bool(all_done.any()):
+        stop = int(all_done.long().argmax())
+        assert gen.shape[1] == stop + 1  # stopped exactly where the per-step loop would
+    else:
+        assert gen.shape[1] == 40
+    # rows that finished are padded after their eos
+    for r in range(2):
+        hit = (gen[r] == eos).nonzero()
+        if len(hit):
+            assert (gen[r, int(hit[0]) + 1:] == cfg.pad_token_id).all()

@@ -6,7 +6,9 @@ by the reference". The base model it extends is pinned by tests/golden. Dropout 
 library's counter-based hash, restated in numpy (oracle lora_keep_mask) and compared bit-exactly.
 
 Tolerances: bf16 storage (2^-8 relative step). Kernel-level outputs max|err| <= 1e-2 * scale;
-model-level loss |d| <= 3e-2, logits / gradients relative-L2 <= 3e-2 / 6e-2 (as tests/test_model_gpu.py).
+model-level (bf16, against the bf16-faithful peft restatement) logits relative-L2 <= 1e-2, loss
+|d| <= 1e-2, every trainable gradient relative-L2 <= 2e-2 (as tests/test_model_gpu.py); the f32
+parity mode at 1e-3 logits / 1e-4 loss / 1e-3 gradients.
 """
 import numpy as np
 import pytest

@@ -112,7 +112,23 @@ def test_forward_backward_matches_reference_golden():
             ours = p.grad.float().norm().item()
             assert abs(ours - ref) <= 3e-2 * ref + 1e-6, (k, ours, ref)
             checked += 1
-    assert checked > 10
+    # element-level: the reference's own sampled fp32 gradients (fixed-stride samples of the large
+    # tensors) against this bf16 path, so a bug shared by the kernels and the bf16-faithful
+    # oracle cannot hide. Cross-precision tolerance: bf16 activations and weights through the
+    # whole backward chain put the sampled elements ~1e-2 away (rel-L2); gate 5e-2.
+    worst, n_el = 0.0, 0
+    for key in g.files:
+        if key.startswith("grad/"):
+            k = key[len("grad/"):]
+            if not params[k].requires_grad:
+                continue
+            stride = int(g["gradstride/" + k][0])
+            ours = params[k].grad.reshape(-1)[::stride].float().cpu()
+            err = rel_l2(ours, g[key])
+            assert err <= 5e-2, (k, err)
+            worst, n_el = max(worst, err), n_el + 1
+    assert checked > 10 and n_el > 0
+    print(f"bf16 vs reference fp32 golden: worst sampled-gradient rel-L2 {worst:.2e} over {n_el} tensors")
 
 
 def test_right_padded_batch_matches_oracle():
@@ -154,7 +170,8 @@ def test_reference_trainable_policy_grads():
 def test_full_size_layer_shapes_run():
     """one full-width Vicuna-7B decoder layer and one CLIP-L layer (B=1) through the whole model
     at config-3 shapes (L = 1088, vocab 32064) fwd+bwd: output shapes, finite loss and non-zero
-    finite gradients. Numerical parity at these widths is tests/test_full_size.py's."""
+    finite gradients, and the forward (logits, loss) against the bf16-faithful oracle at this
+    width; per-layer gradient parity at these widths is tests/test_full_size.py's."""
     from cullavo_amd.config import CuLLaVOConfig, CLIPVisionConfig, LlamaConfig
     from cullavo_amd.arch_cullavo import CuLLaVOModel
     cfg = CuLLaVOConfig(vision_config=CLIPVisionConfig(num_hidden_layers=2),
@@ -168,6 +185,16 @@ def test_full_size_layer_shapes_run():
     out = m(input_ids=ids, pixel_values=pix, attention_mask=torch.ones_like(ids), labels=labels)
     assert out.logits.shape == (1, 1088, 32064)
     assert torch.isfinite(out.loss)
+    # forward parity at full width: the bf16-faithful oracle on the same weights and inputs
+    W = {}
+    for ar in m.arenas.values():
+        W.update({k: v.detach().cpu() for k, v in ar.params.items()})
+    ocfg = O.CuLLaVOCfg(vision=O.VisionCfg(num_hidden_layers=2), text=O.TextCfg(num_hidden_layers=1))
+    with torch.no_grad():
+        loss_ref, logits_ref, _ = O.forward(W, ocfg, ids.cpu(), pix.cpu(), torch.ones_like(ids).cpu(), labels.cpu())
+    err = rel_l2(out.logits.detach()[0], logits_ref[0])
+    assert err <= 1e-2, err
+    assert abs(out.loss.item() - loss_ref.item()) <= 1e-2, (out.loss.item(), loss_ref.item())
     out.loss.backward()
     gflat = m.arenas["layers"].grad_flat
     assert torch.isfinite(gflat.float()).all()

@@ -1,0 +1,11 @@
+#!/bin/bash
+# gpurun, retried only while the pool has no free slot or box (nothing ran, nothing charged)
+out=$1; shift
+for i in 1 2 3 4 5 6 7 8; do
+  timeout 2400 /usr/local/graft/bin/gpurun "$@" > $out 2>&1
+  if grep -q "nothing was charged\|no free box right now" $out && ! grep -q "status=ok" $out; then
+    sleep 150; continue
+  fi
+  break
+done
+tail -80 $out
