@@ -267,6 +267,8 @@ def decode_main(args):
         elapsed = time.perf_counter() - t0
     step_s = elapsed / n_tok
     n_launch = len(gv)
+    if not n_launch or g_ms <= 0:
+        raise RuntimeError("decode bench: no GEMV launch was traced in the eager decode steps")
     achieved = g_bytes / (g_ms * 1e-3) / 1e9
     line = {
         "metric": f"7B KV-cache decode tokens/sec (batch {B}, {L0}-row prompt)", "value": round(B * n_tok / elapsed, 2),

@@ -864,7 +864,7 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
 // makes the N = 4096 products (every dX, o and down forward) 496 tiles = 1.94 rounds instead of
 // 736 192-row tiles = 2.88 rounds.
 enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8, kT288x256 = 10,
-       kTpp4 = 12, kTpp5 = 13 };
+       kTpp4 = 12, kTpp5 = 13, kTpp4x32 = 15, kTpp5x32 = 16 };
 // plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
 double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
@@ -933,7 +933,8 @@ extern "C" int cullavo_gemm_set_streamk(int mode) {
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11 || mode == kTpp4 || mode == kTpp5) ? mode
+  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11 || mode == kTpp4 || mode == kTpp5 ||
+                   mode == kTpp4x32 || mode == kTpp5x32) ? mode
                                                                                                         : -1;
   return prev;
 }
@@ -990,8 +991,8 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
   if ((tile == 7 || tile == 11) && a_layout != 0) tile = 6;
-  static const int bm[14] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288, 256, 256};
-  static const int bn[14] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256};
+  static const int bm[17] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288, 256, 256, 16, 256, 256};
+  static const int bn[17] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 16, 256, 256};
   if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
   (void)b_layout;
   return tile;
@@ -1098,7 +1099,9 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     L8P(1, 1)
 #undef L8P
   }
-  if (tile == kTpp4 || tile == kTpp5) return cvgemm_launch_pp(p, tile == kTpp4 ? 4 : 5, a_layout, b_layout, f32, s);
+  if (tile == kTpp4 || tile == kTpp5 || tile == kTpp4x32 || tile == kTpp5x32)
+    return cvgemm_launch_pp(p, tile == kTpp4 ? 4 : tile == kTpp5 ? 5 : tile == kTpp4x32 ? 14 : 15, a_layout, b_layout,
+                            f32, s);
   if (tile == kT4s) {
 #define L4S(AL, BL) return f32 ? launch4s<AL, BL, CULLAVO_DT_F32>(p, s) : launch4s<AL, BL, CULLAVO_DT_BF16>(p, s);
     if (a_layout == 0 && b_layout == 0) { L4S(0, 0) }

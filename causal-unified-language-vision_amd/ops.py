@@ -155,7 +155,10 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
                  _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _ptr(addend), ld_addend,
                  drop_operand, float(drop_p), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, None, 0, int(f32))
     ws = None
-    if split_k and not f32:
+    # decode rows (M <= 16, forward layouts): the library streams W through its GEMV kernel
+    # (cullavo_gemm_plan tile 14) and takes no split-K workspace
+    gemv = M <= 16 and not f32 and lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None) == 14
+    if split_k and not f32 and not gemv:
         nbytes = lib().cullavo_gemm_workspace(ctypes.addressof(d))
         if nbytes:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=C.device)

@@ -45,9 +45,9 @@ def close(out, ref, tol, what=""):
 GEMM_SHAPES = [(128, 128, 64), (256, 384, 512), (200, 136, 72), (77, 520, 1000), (1024, 1024, 1024)]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, -1],
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 15, 16, -1],
                 ids=["t128", "t256x128", "t256x256", "t192x256", "t8phase", "t8phase10", "t256alt", "t192alt", "t4stage",
-                     "t288x256", "tpp4", "tpp5", "auto"])
+                     "t288x256", "tpp4", "tpp5", "tpp4x32", "tpp5x32", "auto"])
 def tile_mode(request):
     from cullavo_amd import _lib
     prev = _lib.lib().cullavo_gemm_set_tile(request.param)
@@ -243,7 +243,7 @@ def test_gemm_pipelined_repeatable(al, bl):
     back to back at sizes with K tails and several K-tiles, must be bit-identical every time
     (a read racing its LDS-DMA shows up as rare wrong tiles) and match the fp32 product."""
     from cullavo_amd import _lib
-    for mode in (2, 3, 4, 5, 6, 7, 12, 13):
+    for mode in (2, 3, 4, 5, 6, 7, 12, 13, 15, 16):
         prev = _lib.lib().cullavo_gemm_set_tile(mode)
         try:
             for (M, N, K) in [(768, 1024, 4160), (520, 264, 200), (2048, 2048, 1024)]:
