@@ -130,7 +130,63 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs p, int splits) {
 // 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
 // partner wave's MFMAs instead of beside nothing). Data-parallel blocks: one whole tile each,
 // the first sk_dp virtual tiles (all of them without a stream-K tail).
-template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
+// Fused LoRA up-projection (round 4; the reference recipe's peft adapters, cullavo/load_cullavo.py:
+// 94-112): after the main K loop each lane rounds its base outputs v = round(alpha*acc + bias) into
+// packed bf16 registers, the tile's u rows (this N-tile's module block, 64 wide) and lora_B rows
+// are staged by LDS-DMA into the now idle stage 0, one 64-deep MFMA K-tile computes u B^T into the
+// freed accumulators, and acc := v + round(scale * u B^T): the addend of the unfused path, never
+// written to or read back from HBM. The epilogue then runs with alpha 1 and no bias (applied).
+template <int BM2, int BN, int TMW, int TN>
+DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wave, int wm,
+                   int wn, int lane) {
+  constexpr int WN_COLS = BN / 4;
+  uint32_t base[TMW][TN][2];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias && n < p.N) {
+      const u16x4 b4 = *reinterpret_cast<const u16x4*>(p.bias + n);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = bf2f(b4[j]);
+    }
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm) {
+      u16 h[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[j] = f2bf(acc[tm][tn][j] * p.alpha + bv[j]);
+      base[tm][tn][0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      base[tm][tn][1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+    }
+  }
+  const int64_t mod = n0 / p.lora_out;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(p.lora_u + mod * 64, ((p.M - 1) * p.ld_lu + 64) * 2);
+  const __amdgpu_buffer_rsrc_t rbl = make_rsrc(p.lora_b, ((p.N - 1) * 64 + 64) * 2);
+  dma_tile<0, BM2, 8>(ru, p.ld_lu, m0, p.M, 0, 64, smem, wave, lane);
+  dma_tile<0, BN, 8>(rbl, 64, n0, p.N, 0, 64, smem + BM2 * BK * 2, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TMW; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  tile_mfma<0, 0, BM2, BN, TMW, TN>(smem, wm, wn, lane, acc);
+#pragma unroll
+  for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const uint32_t b01 = base[tm][tn][0], b23 = base[tm][tn][1];
+      const float bb[4] = {bf2f((u16)(b01 & 0xFFFF)), bf2f((u16)(b01 >> 16)), bf2f((u16)(b23 & 0xFFFF)),
+                           bf2f((u16)(b23 >> 16))};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[tm][tn][j] = bb[j] + round_bf(acc[tm][tn][j] * p.lora_scale);
+    }
+  __syncthreads();  // every wave's fragment reads of the staged tiles before the epilogue reuses smem
+  p.alpha = 1.f;
+  p.bias = nullptr;
+}
+
+template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0, bool LORA = false>
 __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
   constexpr int WN_COLS = BN / 4;     // per-wave N extent (4 waves across N)
@@ -169,6 +225,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
     return;
   }
   tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, 0, nk_all, smem, wave, lane, acc);
+  if constexpr (LORA) lora_fuse<BM2, BN, TMW, TN>(p, acc, smem, m0, n0, wave, wm, wn, lane);
 
   if constexpr (BN == 256) {
     if (p.epi_lds) {
@@ -769,7 +826,7 @@ float* sk_workspace(hipStream_t s) {
   return (float*)ptr;
 }
 
-template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0>
+template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0, bool LORA = false>
 int launch256(GemmArgs p, hipStream_t s) {
   // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB);
   // then the prefetch's 256-B dummy slot
@@ -777,7 +834,7 @@ int launch256(GemmArgs p, hipStream_t s) {
   const int smem = p.pf_lds + 256;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR>,
+    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -788,7 +845,7 @@ int launch256(GemmArgs p, hipStream_t s) {
     const int splits = (int)cdiv(nk, p.kt_per);
     p.sk_dp = (int)tiles;
     p.sk_units = 0;
-    gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
+    gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
     const int64_t work = p.M * (p.N / 4);
     splitk_reduce_k<CT><<<(int)std::min<int64_t>(cdiv(work, 256), 4096), 256, 0, s>>>(p, splits);
     return cullavo_check_launch("gemm256 split-K");
@@ -811,7 +868,7 @@ int launch256(GemmArgs p, hipStream_t s) {
       p.sk_ws = ws;
     }
   }
-  if (p.sk_dp > 0) gemm256_k<AL, BL, CT, BM2, BN2, LDR><<<p.sk_dp, 512, smem, s>>>(p);
+  if (p.sk_dp > 0) gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA><<<p.sk_dp, 512, smem, s>>>(p);
   if (p.sk_units > 0) {
     static bool sk_attr = false;
     if (!sk_attr) {
@@ -1028,6 +1085,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   CV_REQUIRE(d.drop_operand == 0 || (d.drop_p >= 0.f && d.drop_p < 1.f), CULLAVO_EINVAL, "drop_p must be in [0, 1)");
   CV_REQUIRE(d.drop_operand != 1 || a_layout == 0, CULLAVO_EUNSUPPORTED, "dropout on A needs a_layout 0");
   CV_REQUIRE(d.drop_operand != 2 || b_layout == 1, CULLAVO_EUNSUPPORTED, "dropout on B needs b_layout 1");
+  CV_REQUIRE(d.lora_u == nullptr || !d.f32_operands, CULLAVO_EUNSUPPORTED, "fused LoRA: bf16 operands only");
   if (d.f32_operands) return cullavo_gemm_f32_impl(d, CV_STREAM(stream));  // gemm_f32.hip
   if (M == 0 || N == 0) return CULLAVO_OK;
   const int64_t tm = cdiv(M, BM), tn = cdiv(N, BN);
@@ -1060,11 +1118,30 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.dma_pre = g_dma_pre && (a_layout == 1 || K % BK == 0) && (b_layout == 1 || K % BK == 0);
   p.pf = g_prefetch;
   p.pf_lds = 0;
+  p.lora_u = nullptr;
+  p.lora_b = nullptr;
+  p.ld_lu = 0;
+  p.lora_out = 0;
+  p.lora_scale = 0.f;
   hipStream_t s = CV_STREAM(stream);
   const bool f32 = c_dtype == CULLAVO_DT_F32;
   const int64_t a_ext = a_layout == 0 ? (M - 1) * lda + K : (K - 1) * lda + M;
   const int64_t b_ext = b_layout == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N;
   const bool dma_ok = K > 0 && a_ext * 2 < (int64_t)kOOB && b_ext * 2 < (int64_t)kOOB;
+  if (d.lora_u != nullptr) {  // the LoRA up-projection fused into the 256x256 kernel (lora_fuse)
+    CV_REQUIRE(a_layout == 0 && b_layout == 0 && !f32 && !d.f32_operands && d.lora_b != nullptr &&
+                   d.lora_r == 64 && d.lora_out > 0 && d.lora_out % 256 == 0 && N % d.lora_out == 0 &&
+                   d.ld_lora_u % 8 == 0 && d.ld_lora_u >= (N / d.lora_out) * 64 && d.addend == nullptr &&
+                   d.drop_operand == 0 && d.beta == 0.f && act != CULLAVO_ACT_SWIGLU_BWD && M > 16 && dma_ok,
+               CULLAVO_EUNSUPPORTED, "fused LoRA: a_layout = b_layout = 0, bf16, r = 64, module width a multiple of 256 "
+                                     "dividing N, no addend / dropout / beta, M > 16");
+    p.lora_u = (const u16*)d.lora_u;
+    p.ld_lu = d.ld_lora_u;
+    p.lora_b = (const u16*)d.lora_b;
+    p.lora_out = d.lora_out;
+    p.lora_scale = d.lora_scale;
+    return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, default_ldr<0, 0>(), true>(p, s);
+  }
   // decode rows (M = batch <= 16, Y = X W^T): stream W once through the GEMV kernel (gemv.hip)
   if (gemv_eligible(M, a_layout, b_layout, dropping)) return cvgemm_launch_gemv(p, f32, s);
   bool split256 = false;

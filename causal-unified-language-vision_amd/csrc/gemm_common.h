@@ -44,6 +44,13 @@ struct GemmArgs {
   int dma_pre;        // 8-wave 256-row kernels: per-lane DMA offsets precomputed, K advance in soffset
   int pf;             // 8-wave 256-row kernels: L2 prefetch of K-tile kt+2 (with dma_pre only)
   int pf_lds;         // byte offset of the prefetch's dummy LDS slot (past stages and epilogue image)
+  // fused LoRA up-projection (gemm256_k<..., LORA = true>): t = round(lora_scale * u_m B_m^T) for
+  // the module m = n / lora_out of each output column, added to round(alpha*acc + bias)
+  const u16* lora_u;  // [M, n_mod * 64] (row stride ld_lu): lora_A outputs of the group's modules
+  int64_t ld_lu;
+  const u16* lora_b;  // [N, 64] row-major: the group's lora_B weights stacked in column order
+  int64_t lora_out;   // output columns per module (a multiple of 256)
+  float lora_scale;
 };
 
 template <typename V>

@@ -15,54 +15,78 @@
 // writes C.
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 namespace {
 using namespace cvgemm;
 
 constexpr int kGemvWaves = 8;
-constexpr int kGemvBatch = 16;  // k-steps per load batch
+constexpr int kGemvBatch = 16;  // W fragment loads per batch
+constexpr int kGemvDefault = 1;
 
-template <int CT>
+// ORDER 0: each wave a contiguous K range; ORDER 1: k-steps dealt round-robin over the 8 waves
+// (at any moment a workgroup reads one contiguous 512-B run per weight row); RB: 16-row blocks per
+// workgroup (each wave computes all of them over its k-steps)
+template <int CT, int ORDER, int RB>
 __global__ __launch_bounds__(512, 1) void gemv_k(GemmArgs p) {
-  __shared__ f32x4 red[kGemvWaves][64];
+  __shared__ f32x4 red[kGemvWaves][RB][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n0 = (int64_t)blockIdx.x * 16;
+  const int64_t n0 = (int64_t)blockIdx.x * 16 * RB;
   const int64_t nk = cdiv(p.K, 32);
   const int64_t per = cdiv(nk, kGemvWaves);
-  const int64_t kb = wave * per, ke = min(nk, kb + per);
   const int r = lane & 15, g = lane >> 4;
-  const u16* wrow = p.B + min(n0 + r, p.N - 1) * p.ldb + 8 * g;
+  const u16* wrow[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) wrow[rb] = p.B + min(n0 + 16 * rb + r, p.N - 1) * p.ldb + 8 * g;
   const bool xrow = r < p.M;
   const u16* xp = p.A + (xrow ? r : 0) * p.lda + 8 * g;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t k0 = kb; k0 < ke; k0 += kGemvBatch) {
-    frag8 w[kGemvBatch], x[kGemvBatch];
+  f32x4 acc[RB];
 #pragma unroll
-    for (int i = 0; i < kGemvBatch; ++i) {
-      const int64_t k = (k0 + i) * 32 + 8 * g;  // this lane's first k of step k0 + i
-      const bool in = k0 + i < ke && k < p.K;
-      const int64_t off = in ? (k0 + i) * 32 : 0;
-      w[i] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow + off)) : frag8{};
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NB = kGemvBatch / RB;  // k-steps per batch (W loads per batch stay kGemvBatch)
+  for (int64_t j0 = 0; j0 < per; j0 += NB) {
+    frag8 w[NB][RB], x[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * kGemvWaves + wave;
+      const int64_t kend = ORDER == 0 ? min(nk, (int64_t)(wave + 1) * per) : nk;
+      const int64_t k = ks * 32 + 8 * g;  // this lane's first k of the step
+      const bool in = j0 + i < per && ks < kend && k < p.K;
+      const int64_t off = in ? ks * 32 : 0;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+        w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
       x[i] = (in && xrow) ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(xp + off)) : frag8{};
     }
 #pragma unroll
-    for (int i = 0; i < kGemvBatch; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[i], x[i], acc, 0, 0, 0);
-  }
-  red[wave][lane] = acc;
-  __syncthreads();
-  if (wave == 0) {
-    f32x4 s = red[0][lane];
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
-    for (int w2 = 1; w2 < kGemvWaves; ++w2) s += red[w2][lane];
-    store4<CT>(p, s, r, n0 + 4 * g);
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[i][rb], x[i], acc[rb], 0, 0, 0);
+  }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) red[wave][rb][lane] = acc[rb];
+  __syncthreads();
+  if (wave < RB) {
+    f32x4 s = red[0][wave][lane];
+#pragma unroll
+    for (int w2 = 1; w2 < kGemvWaves; ++w2) s += red[w2][wave][lane];
+    store4<CT>(p, s, r, n0 + 16 * wave + 4 * g);
   }
 }
 
 }  // namespace
 
 int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
-  const unsigned grid = (unsigned)cdiv(p.N, 16);
-  if (f32) gemv_k<CULLAVO_DT_F32><<<grid, 64 * kGemvWaves, 0, s>>>(p);
-  else gemv_k<CULLAVO_DT_BF16><<<grid, 64 * kGemvWaves, 0, s>>>(p);
+  // lab switch (CULLAVO_GEMV: 0 contiguous K ranges, 1 round-robin k-steps, 2 / 3 = 0 / 1 with
+  // 32 rows per workgroup), read once per process
+  static const int v = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : kGemvDefault;
+  const int rb = (v & 2) ? 2 : 1;
+  const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
+#define GV(O, R)                                                                                      \
+  if (f32) gemv_k<CULLAVO_DT_F32, O, R><<<grid, 64 * kGemvWaves, 0, s>>>(p);                            \
+  else gemv_k<CULLAVO_DT_BF16, O, R><<<grid, 64 * kGemvWaves, 0, s>>>(p);
+  if (v == 0) { GV(0, 1) } else if (v == 1) { GV(1, 1) } else if (v == 2) { GV(0, 2) } else { GV(1, 2) }
+#undef GV
   return cullavo_check_launch("gemv");
 }

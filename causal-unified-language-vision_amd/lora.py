@@ -124,6 +124,27 @@ def module_seed(step_seed: int, uid: int, m: int) -> int:
     return (x * 0x94D049BB133111EB) & _M64
 
 
+class LoraTerm:
+    """The adapters' share t = scaling * u_m B_m^T of a group's Linear outputs, not yet computed.
+    ops.linear fuses it into the base GEMM (cullavo_gemm_desc.lora_*: one 64-deep MFMA K-tile
+    after the main loop, t added with peft's roundings and never written to HBM) when the library
+    supports the shape, and calls materialize() (the separate r = 64 GEMMs) otherwise."""
+
+    def __init__(self, group, u):
+        self.group, self.u = group, u
+
+    def fused_args(self, M: int, N: int):
+        g = self.group
+        w = g.outs[0]
+        if (g.r != 64 or M <= 16 or N != g.out_total or any(o != w for o in g.outs) or w % 256
+                or self.u.dtype != torch.bfloat16 or ops._ld(self.u) % 8):
+            return None
+        return self.u, g.b_stack(), w, g.scaling
+
+    def materialize(self):
+        return self.group.up_project(self.u)
+
+
 class LoraGroup:
     """The LoRA adapters of the Linears that share one input (see the module docstring)."""
 
@@ -171,11 +192,19 @@ class LoraGroup:
                             drop_seed=module_seed(step_seed, self.uid, m))
         else:
             ops.gemm_ex(0, 0, M, R, self.in_f, x, ldx, self.a_stack(), self.in_f, u, R)
-        t = torch.empty((M, self.out_total), dtype=x.dtype, device=x.device)
+        return LoraTerm(self, u), u
+
+    def up_project(self, u):
+        """t [M, out_total] = scaling * u_m B_m^T per module block (the unfused addend)"""
+        M, r, R = u.shape[0], self.r, self.n * self.r
+        t = torch.empty((M, self.out_total), dtype=u.dtype, device=u.device)
         for m in range(self.n):
             ops.gemm_ex(0, 0, M, self.outs[m], r, u[:, m * r:], R, self.B(m), r, t[:, self.offs[m]:], self.out_total,
                         alpha=self.scaling)
-        return t, u
+        return t
+
+    def b_stack(self):
+        return self.arena.view(self.b_keys[0], (self.out_total, self.r))
 
     def backward(self, dy, x, u, dx, train: bool, step_seed: int):
         """Writes dA / dB into the arena's gradient slots and accumulates the adapters' share of

@@ -8,6 +8,7 @@ the CPU: every function requires CUDA(HIP) tensors and fails loudly otherwise.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -133,19 +134,25 @@ class GemmDesc(ctypes.Structure):
                 ("ldr", ctypes.c_int64), ("beta", ctypes.c_float), ("addend", ctypes.c_void_p),
                 ("ld_addend", ctypes.c_int64), ("drop_operand", ctypes.c_int), ("drop_p", ctypes.c_float),
                 ("drop_seed", ctypes.c_uint64), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
-                ("f32_operands", ctypes.c_int)]
+                ("f32_operands", ctypes.c_int), ("lora_u", ctypes.c_void_p), ("ld_lora_u", ctypes.c_int64),
+                ("lora_b", ctypes.c_void_p), ("lora_out", ctypes.c_int64), ("lora_r", ctypes.c_int),
+                ("lora_scale", ctypes.c_float)]
 
 
 DROP_NONE, DROP_A, DROP_B, DROP_OUT = 0, 1, 2, 3
 SMALL_M = 256  # Linear calls with at most this many rows (KV-cache decode) may run split-K
+# the LoRA up-projection fused into the base GEMM (cullavo_gemm_desc.lora_*): on by default; the
+# unfused path (t materialised by its own GEMMs, added as `addend`) stays for A/B and ineligible shapes
+LORA_FUSE = os.environ.get("CULLAVO_LORA_FUSE", "1") != "0"
 
 
 def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,
             alpha: float = 1.0, bias=None, act: int = ACT_NONE, preact=None, residual=None, ldr: int = 0,
             beta: float = 0.0, addend=None, ld_addend: int = 0, drop_operand: int = DROP_NONE,
-            drop_p: float = 0.0, drop_seed: int = 0, split_k: bool = True):
+            drop_p: float = 0.0, drop_seed: int = 0, split_k: bool = True, lora=None):
     """cullavo_gemm_ex: gemm() plus the LoRA addend, dropout masks and split-K (see the header).
-    The split-K workspace comes from torch's caching allocator (kernels never allocate)."""
+    The split-K workspace comes from torch's caching allocator (kernels never allocate).
+    lora = (u, b_stack, module_width, scale): the fused LoRA up-projection (ABI 3 desc fields)."""
     _dev(A, B, C, bias, preact, residual, addend)
     f32 = A.dtype == torch.float32
     for t in (B, C, bias, preact, residual, addend):
@@ -154,6 +161,12 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
     d = GemmDesc(a_layout, b_layout, M, N, K, _ptr(A), lda, _ptr(B), ldb, _ptr(C), ldc, _dt(C), float(alpha),
                  _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _ptr(addend), ld_addend,
                  drop_operand, float(drop_p), int(drop_seed) & 0xFFFFFFFFFFFFFFFF, None, 0, int(f32))
+    if lora is not None:
+        u, bst, width, scale = lora
+        _dev(u, bst)
+        d.lora_u, d.ld_lora_u, d.lora_b, d.lora_out = _ptr(u), _ld(u), _ptr(bst), int(width)
+        d.lora_r, d.lora_scale = int(bst.shape[1]), float(scale)
+        split_k = False
     ws = None
     # decode rows (M <= 16, forward layouts): the library streams W through its GEMV kernel
     # (cullavo_gemm_plan tile 14) and takes no split-K workspace
@@ -179,7 +192,9 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
 def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: bool = False, out=None,
            addend=None):
     """y = act(x @ w.T + bias [+ addend]) (+ residual); x [M,K] (row stride may exceed K), w [N,K].
-    addend [M,N] is the LoRA term, added after the bias with peft's roundings."""
+    addend [M,N] is the LoRA term, added after the bias with peft's roundings; it may also be a
+    lora.LoraTerm (the adapters' u, not yet multiplied by lora_B), which the base GEMM fuses when
+    the library can (lora_fusable) and which is materialised otherwise."""
     M, K = x.shape
     N = w.shape[0]
     if w.shape[1] != K:
@@ -187,6 +202,13 @@ def linear(x, w, bias=None, *, act: int = ACT_NONE, residual=None, want_preact: 
     y = out if out is not None else torch.empty((M, N), dtype=x.dtype, device=x.device)
     pre = torch.empty((M, N), dtype=x.dtype, device=x.device) if want_preact else None
     ldr = _ld(residual) if residual is not None else 0
+    if addend is not None and hasattr(addend, "fused_args"):
+        fa = addend.fused_args(M, N) if LORA_FUSE and x.dtype == torch.bfloat16 else None
+        if fa is not None:
+            gemm_ex(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
+                    residual=residual, ldr=ldr, lora=fa)
+            return (y, pre) if want_preact else y
+        addend = addend.materialize()
     if addend is None and M > SMALL_M:
         gemm(0, 0, M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, act=act, preact=pre,
              residual=residual, ldr=ldr)

@@ -51,7 +51,7 @@ extern "C" {
 /* ABI version: bumped whenever an exported signature changes (2: cullavo_im2col_patches gained
    out_dtype, cullavo_vision_embed_ln dtype, cullavo_gemm_desc f32_operands). A consumer built
    against this header checks cullavo_abi_version() == CULLAVO_ABI_VERSION at load. */
-#define CULLAVO_ABI_VERSION 2
+#define CULLAVO_ABI_VERSION 3
 
 int cullavo_abi_version(void);
 const char* cullavo_last_error(void);
@@ -117,6 +117,19 @@ typedef struct {
   int f32_operands;         /* 0 (default): A, B, bias, residual, preact, addend bf16;
                                1: every operand and C f32, nothing rounded (the f32 parity
                                mode: an exact f32 MFMA chain, v_mfma_f32_16x16x4_f32) */
+  /* ABI 3: the LoRA up-projection fused into the base product (nullable lora_u). For output
+   * column n of module m = n / lora_out the kernel adds t = round(lora_scale * u_m . B[n]) with
+   * u_m = lora_u[row][m*64 .. m*64+63] (row stride ld_lora_u) and B[n] = lora_b[n][0..63]
+   * (the group's lora_B weights stacked, [N, 64]), exactly where `addend` would be added (the
+   * same roundings: v = round(round(alpha*A.B^T + bias) + t)); t is never written to memory.
+   * Needs a_layout = b_layout = 0, bf16 operands and output, lora_r = 64, lora_out a multiple of
+   * 256 dividing N, no addend / dropout / beta, M > 16; otherwise CULLAVO_EUNSUPPORTED. */
+  const void* lora_u;
+  int64_t ld_lora_u;
+  const void* lora_b;
+  int64_t lora_out;
+  int lora_r;
+  float lora_scale;
 } cullavo_gemm_desc;
 int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream);
 /* sizeof(cullavo_gemm_desc) as compiled into the library (binding check) */

@@ -186,7 +186,8 @@ def test_lora_group_forward_backward(train):
     ar, grp, s, names = _lora_arena(n, out, inn, r, 40)
     step_seed = 987654321
     x = rnd((T, inn), 50)
-    t, u = grp.forward(x.cuda(), train, step_seed)
+    term, u = grp.forward(x.cuda(), train, step_seed)
+    t = term.materialize()
     dy = rnd((T, n * out), 51)
     dx = torch.zeros((T, inn), dtype=BF, device="cuda")
     ar.zero_grad()
@@ -211,6 +212,55 @@ def test_lora_group_forward_backward(train):
     for m, nm in enumerate(names):
         close(ar.params[f"L.self_attn.{nm}.lora_A.step1.weight"].grad, As[m].grad, 1.5e-2, f"dA {nm}")
         close(ar.params[f"L.self_attn.{nm}.lora_B.step1.weight"].grad, Bs[m].grad, 1.5e-2, f"dB {nm}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,epi", [(600, "bias"), (1031, "res"), (256, "qgelu_pre"), (4100, "none")])
+def test_lora_fused_into_base_gemm(T, epi):
+    """The LoRA up-projection fused into the base GEMM (cullavo_gemm_desc.lora_*: one 64-deep MFMA
+    K-tile after the main loop, t = round(scale * u B^T) added to round(x W^T + b) in registers)
+    against the unfused path (t by its own GEMMs, read back as the addend): the same roundings, so
+    at most one bf16 step apart (the r = 64 sums may associate differently), and against the fp32
+    peft restatement. Ragged M tiles, 3 modules of 256 columns, bias / residual / quick_gelu with
+    the pre-activation stored."""
+    from cullavo_amd import ops
+    from cullavo_amd.ops import ACT_QUICK_GELU
+    inn, out, r, n = 512, 256, 64, 3
+    ar, grp, s, names = _lora_arena(n, out, inn, r, 60)
+    x = rnd((T, inn), 61).cuda()
+    W = rnd((n * out, inn), 62, inn ** -0.5).cuda()
+    bias = rnd((n * out,), 63).cuda() if epi in ("bias", "qgelu_pre") else None
+    res = rnd((T, n * out), 64).cuda() if epi == "res" else None
+    act = ACT_QUICK_GELU if epi == "qgelu_pre" else 0
+    term, u = grp.forward(x, False, 0)
+    assert term.fused_args(T, n * out) is not None
+    outs = {}
+    for fuse in (True, False):
+        prev = ops.LORA_FUSE
+        ops.LORA_FUSE = fuse
+        try:
+            y = ops.linear(x, W, bias, act=act, residual=res, want_preact=act != 0, addend=term)
+        finally:
+            ops.LORA_FUSE = prev
+        outs[fuse] = y if isinstance(y, tuple) else (y, None)
+    torch.cuda.synchronize()
+    for a, b in zip(outs[True], outs[False]):
+        if a is None:
+            continue
+        d = (a.float() - b.float()).abs()
+        assert d.max().item() <= 2 ** -7 * max(1.0, b.float().abs().max().item()), d.max().item()
+        assert (d != 0).float().mean().item() < 0.01
+    # fp32 restatement: round(round(x W^T + b) + round(scale * u B^T)) (+ residual / act)
+    Bst = grp.b_stack().float().cpu()
+    uc = u.float().cpu()
+    tt = torch.cat([uc[:, m * r:(m + 1) * r] @ Bst[m * out:(m + 1) * out].T for m in range(n)], 1) * s.scaling
+    z = x.float().cpu() @ W.float().cpu().T + (bias.float().cpu() if bias is not None else 0)
+    z = z.to(BF).float() + tt.to(BF).float()
+    if act:
+        z = O.quick_gelu(z.to(BF).float())
+    if res is not None:
+        z = z.to(BF).float() + res.float().cpu()
+    close(outs[True][0], z, 1.5e-2, f"fused LoRA {epi}")
 
 
 def _lora_oracle_masks(model, sctx_seed, n_tokens):
