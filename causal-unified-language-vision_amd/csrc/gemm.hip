@@ -140,7 +140,15 @@ template <int BM2, int BN, int TMW, int TN>
 DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wave, int wm,
                    int wn, int lane) {
   constexpr int WN_COLS = BN / 4;
-  uint32_t base[TMW][TN][2];
+  const int64_t mod = n0 / p.lora_out;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(p.lora_u + mod * 64, ((p.M - 1) * p.ld_lu + 64) * 2);
+  const __amdgpu_buffer_rsrc_t rbl = make_rsrc(p.lora_b, ((p.N - 1) * 64 + 64) * 2);
+  dma_tile<0, BM2, 8>(ru, p.ld_lu, m0, p.M, 0, 64, smem, wave, lane);
+  dma_tile<0, BN, 8>(rbl, 64, n0, p.N, 0, 64, smem + BM2 * BK * 2, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // one 16-column group at a time, so only that group's rounded base outputs (TMW x 2 packed
+  // registers) live beside the accumulators: the 288-row tile fits without spilling
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
@@ -150,37 +158,33 @@ DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) bv[j] = bf2f(b4[j]);
     }
+    uint32_t base[TMW][2];
 #pragma unroll
     for (int tm = 0; tm < TMW; ++tm) {
       u16 h[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) h[j] = f2bf(acc[tm][tn][j] * p.alpha + bv[j]);
-      base[tm][tn][0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-      base[tm][tn][1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      base[tm][0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      base[tm][1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  }
-  const int64_t mod = n0 / p.lora_out;
-  const __amdgpu_buffer_rsrc_t ru = make_rsrc(p.lora_u + mod * 64, ((p.M - 1) * p.ld_lu + 64) * 2);
-  const __amdgpu_buffer_rsrc_t rbl = make_rsrc(p.lora_b, ((p.N - 1) * 64 + 64) * 2);
-  dma_tile<0, BM2, 8>(ru, p.ld_lu, m0, p.M, 0, 64, smem, wave, lane);
-  dma_tile<0, BN, 8>(rbl, 64, n0, p.N, 0, 64, smem + BM2 * BK * 2, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < TMW; ++i)
+    for (int ks = 0; ks < 2; ++ks) {
+      const frag8 fb = read_frag<0>(smem + BM2 * BK * 2, wn * WN_COLS + tn * 16, ks, lane);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  tile_mfma<0, 0, BM2, BN, TMW, TN>(smem, wm, wn, lane, acc);
+      for (int tm = 0; tm < TMW; ++tm) {
+        const frag8 fa = read_frag<0>(smem, wm * (BM2 / 2) + tm * 16, ks, lane);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc[tm][tn], 0, 0, 0);
+      }
+    }
 #pragma unroll
-  for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const uint32_t b01 = base[tm][tn][0], b23 = base[tm][tn][1];
-      const float bb[4] = {bf2f((u16)(b01 & 0xFFFF)), bf2f((u16)(b01 >> 16)), bf2f((u16)(b23 & 0xFFFF)),
-                           bf2f((u16)(b23 >> 16))};
+    for (int tm = 0; tm < TMW; ++tm) {
+      const float bb[4] = {bf2f((u16)(base[tm][0] & 0xFFFF)), bf2f((u16)(base[tm][0] >> 16)),
+                           bf2f((u16)(base[tm][1] & 0xFFFF)), bf2f((u16)(base[tm][1] >> 16))};
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[tm][tn][j] = bb[j] + round_bf(acc[tm][tn][j] * p.lora_scale);
     }
+  }
   __syncthreads();  // every wave's fragment reads of the staged tiles before the epilogue reuses smem
   p.alpha = 1.f;
   p.bias = nullptr;
@@ -1140,6 +1144,9 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     p.lora_b = (const u16*)d.lora_b;
     p.lora_out = d.lora_out;
     p.lora_scale = d.lora_scale;
+    // the 288-row tile where the plan takes it (the N = 4096 products: 2 rounds instead of 3)
+    if (choose_tile(M, N, K, 0, g_force_tile) == kT288x256)
+      return launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1, true>(p, s);
     return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, default_ldr<0, 0>(), true>(p, s);
   }
   // decode rows (M = batch <= 16, Y = X W^T): stream W once through the GEMV kernel (gemv.hip)

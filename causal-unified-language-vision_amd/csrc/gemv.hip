@@ -24,14 +24,65 @@ constexpr int kGemvWaves = 8;
 constexpr int kGemvBatch = 16;  // W fragment loads per batch
 constexpr int kGemvDefault = 1;
 
+// Decode-row input transforms fused into the X fragment loads (cullavo_decode_linear): XF 0 none;
+// 1 RMSNorm (x: the residual stream h [M, K]; each workgroup recomputes the M row statistics with
+// rmsnorm_fwd_k's exact arithmetic, norms.hip, then x = bf16(w * bf16(h * rstd)) per element); 2
+// SwiGLU (x: gate | up [M, 2K]; x = bf16(bf16(silu(g)) * u) as swiglu_fwd_k, elementwise.hip).
+// Either way the values are bitwise those of the unfused kernels, without their launches.
+DEV float gemv_silu(float x) { return x / (1.f + __expf(-x)); }
+
+struct GemvArgs {
+  GemmArgs g;
+  const u16* xf_w;  // RMSNorm weight [K]
+  float xf_eps;
+};
+
+template <int XF>
+DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, float rstd) {
+  const u16x8 xv = *reinterpret_cast<const u16x8*>(xp + off);
+  if (XF == 0) return __builtin_bit_cast(frag8, xv);
+  u16x8 o;
+  if (XF == 1) {
+    const u16x8 wv = *reinterpret_cast<const u16x8*>(a.xf_w + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wv[j]) * round_bf(bf2f(xv[j]) * rstd));
+  } else {
+    const u16x8 uv = *reinterpret_cast<const u16x8*>(xp + off + a.g.K);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(gemv_silu(bf2f(xv[j]))) * bf2f(uv[j]));
+  }
+  return __builtin_bit_cast(frag8, o);
+}
+
 // ORDER 0: each wave a contiguous K range; ORDER 1: k-steps dealt round-robin over the 8 waves
 // (at any moment a workgroup reads one contiguous 512-B run per weight row); RB: 16-row blocks per
-// workgroup (each wave computes all of them over its k-steps)
-template <int CT, int ORDER, int RB>
-__global__ __launch_bounds__(512, 1) void gemv_k(GemmArgs p) {
+// workgroup (each wave computes all of them over its k-steps). Measured alike on the 7B decode
+// step (ORDER 0 / 1: 4.14 / 4.16 ms per token; RB 2: 4.66-4.79, profiles/r04/decode/).
+template <int CT, int ORDER, int RB, int XF>
+__global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
+  const GemmArgs& p = a.g;
   __shared__ f32x4 red[kGemvWaves][RB][64];
+  __shared__ float rs[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (XF == 1) {  // row statistics of rmsnorm_fwd_k (one wave per row, the same summation order)
+    for (int row = wave; row < p.M; row += kGemvWaves) {
+      const u16* xr = p.A + row * p.lda;
+      float ss = 0.f;
+      for (int c = 0; c * 512 < p.K; ++c) {
+        const int col = c * 512 + lane * 8;
+        if (col < p.K) {
+          float v[8];
+          load8(xr + col, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+        }
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) rs[row] = rsqrtf(ss / (float)p.K + a.xf_eps);
+    }
+    __syncthreads();
+  }
   const int64_t n0 = (int64_t)blockIdx.x * 16 * RB;
   const int64_t nk = cdiv(p.K, 32);
   const int64_t per = cdiv(nk, kGemvWaves);
@@ -41,6 +92,7 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemmArgs p) {
   for (int rb = 0; rb < RB; ++rb) wrow[rb] = p.B + min(n0 + 16 * rb + r, p.N - 1) * p.ldb + 8 * g;
   const bool xrow = r < p.M;
   const u16* xp = p.A + (xrow ? r : 0) * p.lda + 8 * g;
+  const float rstd = (XF == 1 && xrow) ? rs[r] : 0.f;
   f32x4 acc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -57,7 +109,7 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemmArgs p) {
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
         w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
-      x[i] = (in && xrow) ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(xp + off)) : frag8{};
+      x[i] = (in && xrow) ? gemv_xfrag<XF>(a, xp, off, k, rstd) : frag8{};
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
@@ -83,10 +135,44 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   static const int v = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : kGemvDefault;
   const int rb = (v & 2) ? 2 : 1;
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
+  GemvArgs a{};
+  a.g = p;
 #define GV(O, R)                                                                                      \
-  if (f32) gemv_k<CULLAVO_DT_F32, O, R><<<grid, 64 * kGemvWaves, 0, s>>>(p);                            \
-  else gemv_k<CULLAVO_DT_BF16, O, R><<<grid, 64 * kGemvWaves, 0, s>>>(p);
+  if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);                         \
+  else gemv_k<CULLAVO_DT_BF16, O, R, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);
   if (v == 0) { GV(0, 1) } else if (v == 1) { GV(1, 1) } else if (v == 2) { GV(0, 2) } else { GV(1, 2) }
 #undef GV
   return cullavo_check_launch("gemv");
+}
+
+extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
+                                     const void* norm_w, float eps, const void* W, int64_t ldw, void* y,
+                                     int64_t ldy, const void* residual, int64_t ldr, void* stream) {
+  CV_REQUIRE(x_transform >= 0 && x_transform <= 2, CULLAVO_EINVAL, "decode_linear: x_transform 0, 1 or 2");
+  CV_REQUIRE(M >= 1 && M <= 16 && N > 0 && K > 0, CULLAVO_EINVAL, "decode_linear: 1 <= M <= 16 rows, N, K > 0");
+  CV_REQUIRE(N % 8 == 0 && K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldy % 8 == 0 &&
+                 (residual == nullptr || ldr % 8 == 0),
+             CULLAVO_EINVAL, "decode_linear: sizes and strides must be multiples of 8");
+  CV_REQUIRE(ldw >= K && ldy >= N && ldx >= (x_transform == 2 ? 2 * K : K) && (residual == nullptr || ldr >= N),
+             CULLAVO_EINVAL, "decode_linear: leading dimension too small");
+  CV_REQUIRE(x_transform != 1 || (norm_w != nullptr && K <= 8192), CULLAVO_EINVAL,
+             "decode_linear: RMSNorm needs its weight and K <= 8192");
+  hipStream_t s = CV_STREAM(stream);
+  GemvArgs a{};
+  GemmArgs& p = a.g;
+  p.A = (const u16*)x;
+  p.B = (const u16*)W;
+  p.C = y;
+  p.residual = (const u16*)residual;
+  p.M = M; p.N = N; p.K = K; p.lda = ldx; p.ldb = ldw; p.ldc = ldy; p.ldr = ldr;
+  p.alpha = 1.f;
+  p.beta = 0.f;
+  p.act = CULLAVO_ACT_NONE;
+  a.xf_w = (const u16*)norm_w;
+  a.xf_eps = eps;
+  const unsigned grid = (unsigned)cdiv(N, 16);
+  if (x_transform == 0) gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  else if (x_transform == 1) gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  else gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 2><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  return cullavo_check_launch("decode_linear");
 }

@@ -22,6 +22,7 @@ import torch
 
 from . import ops
 from .functions import StepContext
+from .lora import NO_LORA
 
 
 class KVCache:
@@ -114,9 +115,16 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
     lg = layer.lora_groups
     B = sctx.B
-    x1, _ = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
-    t, _ = lg["qkv"].forward(x1, False, 0)
-    qkv = ops.linear(x1, layer.w_qkv(), addend=t)
+    # one row per sequence and no adapters: the norms and the SwiGLU run inside the weight-streaming
+    # products (cullavo_decode_linear), bitwise the unfused kernels' values
+    fused = Lnew == 1 and h.shape[0] <= 16 and h.dtype == torch.bfloat16 and all(g is NO_LORA for g in lg.values())
+    if fused:
+        qkv = ops.decode_linear(h, layer.w_qkv(), transform=1, norm_w=layer.input_layernorm.weight,
+                                eps=cfg.rms_norm_eps)
+    else:
+        x1, _ = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
+        t, _ = lg["qkv"].forward(x1, False, 0)
+        qkv = ops.linear(x1, layer.w_qkv(), addend=t)
     q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
     ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
     ops.kv_append(k, v, cache.k[li], cache.v[li], start, B=B, Lnew=Lnew)
@@ -129,6 +137,10 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
                             scale=D ** -0.5, kv_start=sctx.kv_start)
     t, _ = lg["o"].forward(o, False, 0)
     h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h, addend=t)
+    if fused:
+        gu = ops.decode_linear(h2, layer.w_gu(), transform=1, norm_w=layer.post_attention_layernorm.weight,
+                               eps=cfg.rms_norm_eps)
+        return ops.decode_linear(gu, layer.mlp.down_proj.weight, transform=2, residual=h2)
     x2, _ = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
     t, _ = lg["gu"].forward(x2, False, 0)
     gu = ops.linear(x2, layer.w_gu(), addend=t)

@@ -338,6 +338,18 @@ def swiglu_fwd(gu):
     return out
 
 
+def decode_linear(x, w, *, transform: int = 0, norm_w=None, eps: float = 0.0, residual=None):
+    """Decode rows (M <= 16) through cullavo_decode_linear: y = T(x) @ w.T (+ residual) with T the
+    fused input transform (0 none, 1 RMSNorm with norm_w / eps, 2 SwiGLU of x = gate|up [M, 2K])."""
+    _dev(x, w, norm_w, residual)
+    M = x.shape[0]
+    N, K = w.shape
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    call("decode_linear", int(transform), M, N, K, _ptr(x), _ld(x), _ptr(norm_w), float(eps), _ptr(w), _ld(w),
+         _ptr(y), _ld(y), _ptr(residual), _ld(residual) if residual is not None else 0, _stream())
+    return y
+
+
 def swiglu_bwd(dout, gu):
     _dev(dout, gu)
     rows, F2 = gu.shape

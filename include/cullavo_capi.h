@@ -324,6 +324,17 @@ int cullavo_attn_set_rescale(float threshold, float* previous);
 int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, void* k_cache, void* v_cache,
                       int64_t ld_tok, int64_t ld_batch, const int32_t* start, int B, int Lnew, int64_t hd,
                       void* stream);
+/* Decode-step Linear over M <= 16 rows (one token per sequence; reference: the cached forward's
+ * decoder layer, cullavo/arch_cullavo.py:605-636) with its input transform fused into the weight
+ * stream (csrc/gemv.hip): y[M,N] = X W^T (+ residual), W [N,K] bf16 (ldw), where X is
+ *   x_transform 0: x [M,K] as given;
+ *   1: RMSNorm(x; norm_w, eps) of x [M,K] (the residual stream: replaces cullavo_rmsnorm_fwd
+ *      + cullavo_gemm, the values bitwise those of cullavo_rmsnorm_fwd);
+ *   2: SwiGLU of x = gate|up [M,2K] (replaces cullavo_swiglu_fwd + cullavo_gemm, bitwise).
+ * bf16 only; the result is rounded like cullavo_gemm's (residual added after rounding). */
+int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
+                          const void* norm_w, float eps, const void* W, int64_t ldw, void* y, int64_t ldy,
+                          const void* residual, int64_t ldr, void* stream);
 size_t cullavo_attn_decode_workspace(int B, int H, int max_len, int D);
 int cullavo_attn_decode(const void* q, int64_t ldq, const void* k_cache, const void* v_cache, int64_t ld_tok,
                         int64_t ld_batch, const int32_t* kv_len, const int32_t* kv_start, void* o, int64_t ldo,

@@ -291,3 +291,34 @@ def test_generate_eos_stop_with_sparse_checks():
         hit = (gen[r] == eos).nonzero()
         if len(hit):
             assert (gen[r, int(hit[0]) + 1:] == cfg.pad_token_id).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+def test_decode_linear_fused_transforms_bitwise(M):
+    """cullavo_decode_linear's fused input transforms give bitwise the unfused path's values:
+    RMSNorm (cullavo_rmsnorm_fwd then the GEMV) and SwiGLU (cullavo_swiglu_fwd then the GEMV), with
+    and without a residual; plus the plain GEMV against fp32."""
+    from cullavo_amd import ops
+    g = torch.Generator().manual_seed(40 + M)
+    d, F = 4096, 11008
+    h = (torch.randn(M, d, generator=g) * 3).to(BF).cuda()
+    nw = (1 + 0.1 * torch.randn(d, generator=g)).to(BF).cuda()
+    Wq = (torch.randn(3 * 1024, d, generator=g) * d ** -0.5).to(BF).cuda()
+    gu = torch.randn(M, 2 * F, generator=g).to(BF).cuda()
+    Wd = (torch.randn(d, F, generator=g) * F ** -0.5).to(BF).cuda()
+    res = torch.randn(M, d, generator=g).to(BF).cuda()
+    x1, _ = ops.rmsnorm_fwd(h, nw, 1e-5)
+    a = ops.decode_linear(h, Wq, transform=1, norm_w=nw, eps=1e-5)
+    b = ops.decode_linear(x1, Wq)
+    assert torch.equal(a, b)
+    act = ops.swiglu_fwd(gu)
+    for r in (None, res):
+        a = ops.decode_linear(gu, Wd, transform=2, residual=r)
+        b = ops.decode_linear(act, Wd, residual=r)
+        assert torch.equal(a, b)
+    z = x1.float() @ Wq.float().T
+    y = ops.decode_linear(x1, Wq)
+    assert (y.float() - z).abs().max().item() <= 8e-3 * z.abs().max().item()
+    with pytest.raises(ValueError):
+        ops.decode_linear(torch.zeros(17, d, dtype=BF, device="cuda"), Wq)
