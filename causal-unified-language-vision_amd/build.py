@@ -66,12 +66,14 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
         objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH, *objs]
+        tmp = LIB_PATH + ".tmp"  # linked aside, then renamed: a reader never sees a half-written library
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 

@@ -137,16 +137,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs p, int splits) {
 // freed accumulators, and acc := v + round(scale * u B^T): the addend of the unfused path, never
 // written to or read back from HBM. The epilogue then runs with alpha 1 and no bias (applied).
 template <int BM2, int BN, int TMW, int TN>
-DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wave, int wm,
-                   int wn, int lane) {
+DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int staged, int64_t m0, int64_t n0, int wave,
+                   int wm, int wn, int lane) {
   constexpr int WN_COLS = BN / 4;
-  const int64_t mod = n0 / p.lora_out;
-  const __amdgpu_buffer_rsrc_t ru = make_rsrc(p.lora_u + mod * 64, ((p.M - 1) * p.ld_lu + 64) * 2);
-  const __amdgpu_buffer_rsrc_t rbl = make_rsrc(p.lora_b, ((p.N - 1) * 64 + 64) * 2);
-  dma_tile<0, BM2, 8>(ru, p.ld_lu, m0, p.M, 0, 64, smem, wave, lane);
-  dma_tile<0, BN, 8>(rbl, 64, n0, p.N, 0, 64, smem + BM2 * BK * 2, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (staged < 0) {  // not staged by the main loop (its fallback path): stage now
+    lora_stage<BM2, BN>(p, m0, n0, smem, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    smem += staged;  // staged by the last K-tile's iteration, waited for and barriered by the loop
+  }
   // one 16-column group at a time, so only that group's rounded base outputs (TMW x 2 packed
   // registers) live beside the accumulators: the 288-row tile fits without spilling
 #pragma unroll
@@ -228,8 +228,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
     }
     return;
   }
-  tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, 0, nk_all, smem, wave, lane, acc);
-  if constexpr (LORA) lora_fuse<BM2, BN, TMW, TN>(p, acc, smem, m0, n0, wave, wm, wn, lane);
+  const int staged = tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN, LORA>(p, ra, rb, m0, n0, 0, nk_all, smem, wave,
+                                                                       lane, acc);
+  if constexpr (LORA) lora_fuse<BM2, BN, TMW, TN>(p, acc, smem, staged, m0, n0, wave, wm, wn, lane);
 
   if constexpr (BN == 256) {
     if (p.epi_lds) {

@@ -649,9 +649,23 @@ DEV void tile_mfma(const char* cur_c, int wm, int wn, int lane, f32x4 (&acc)[TMW
 // partner wave's MFMAs instead of beside nothing).
 // One tile's K-tiles [kb, ke) into acc (zeroed here): LDS-DMA double buffer, one barrier per
 // K-tile, the MFMA loop of the 8-wave kernels (shared by the data-parallel and stream-K kernels)
-template <int AL, int BL, int BM2, int BN, int LDR, int TMW, int TN>
-DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int64_t m0,
-                      int64_t n0, int kb, int ke, char* smem, int wave, int lane, f32x4 (&acc)[TMW][TN]) {
+// the fused LoRA's operand tiles (module m = n0 / lora_out): u rows m0.. at column block 64 m and
+// lora_B rows n0.., as a 64-deep layout-0 A / B image pair at lds (all eight waves issue)
+template <int BM2, int BN>
+DEV void lora_stage(const GemmArgs& p, int64_t m0, int64_t n0, char* lds, int wave, int lane) {
+  const int64_t mod = n0 / p.lora_out;
+  const __amdgpu_buffer_rsrc_t ru = make_rsrc(p.lora_u + mod * 64, ((p.M - 1) * p.ld_lu + 64) * 2);
+  const __amdgpu_buffer_rsrc_t rbl = make_rsrc(p.lora_b, ((p.N - 1) * 64 + 64) * 2);
+  dma_tile<0, BM2, 8>(ru, p.ld_lu, m0, p.M, 0, 64, lds, wave, lane);
+  dma_tile<0, BN, 8>(rbl, 64, n0, p.N, 0, 64, lds + BM2 * BK * 2, wave, lane);
+}
+
+// LPF (the fused-LoRA kernels, gemm.hip lora_fuse): the last K-tile's iteration stages the
+// adapters' u rows and lora_B rows (a 64-deep layout-0 tile pair) into the stage it frees, so they
+// land under the last MFMAs; returns that stage's offset (-1 when not staged)
+template <int AL, int BL, int BM2, int BN, int LDR, int TMW, int TN, bool LPF = false>
+DEV int tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int64_t m0,
+                     int64_t n0, int kb, int ke, char* smem, int wave, int lane, f32x4 (&acc)[TMW][TN]) {
   constexpr int TILE_A = BM2 * BK * 2;
   constexpr int TILE_B = BN * BK * 2;
   constexpr int STAGE = TILE_A + TILE_B;
@@ -686,6 +700,9 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
         dma_issue<BM2, NWL>(ra, va, dma_soff<AL>(k1, p.lda), nxt, lw);
         dma_issue<BN, NWL>(rb, vb, dma_soff<BL>(k1, p.ldb), nxt + TILE_A, lw);
       }
+      if constexpr (LPF) {
+        if (kt + 1 == ke) lora_stage<BM2, BN>(p, m0, n0, nxt, wave, lane);
+      }
       const bool pf = p.pf && kt + 2 < ke;  // uniform
       if (pf) {
         const int64_t k2 = (int64_t)(kt + 2) * BK;
@@ -703,7 +720,7 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
+    return LPF ? (int)(((ke - kb) & 1) * STAGE) : -1;
   }
 
   for (int kt = kb; kt < ke; ++kt) {
@@ -730,6 +747,7 @@ DEV void tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buf
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  return -1;
 }
 
 // grouped, XCD-friendly tile order: virtual tile index -> (m0, n0)

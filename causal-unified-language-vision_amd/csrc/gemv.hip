@@ -65,24 +65,6 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
   __shared__ float rs[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (XF == 1) {  // row statistics of rmsnorm_fwd_k (one wave per row, the same summation order)
-    for (int row = wave; row < p.M; row += kGemvWaves) {
-      const u16* xr = p.A + row * p.lda;
-      float ss = 0.f;
-      for (int c = 0; c * 512 < p.K; ++c) {
-        const int col = c * 512 + lane * 8;
-        if (col < p.K) {
-          float v[8];
-          load8(xr + col, v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
-        }
-      }
-      ss = wave_sum(ss);
-      if (lane == 0) rs[row] = rsqrtf(ss / (float)p.K + a.xf_eps);
-    }
-    __syncthreads();
-  }
   const int64_t n0 = (int64_t)blockIdx.x * 16 * RB;
   const int64_t nk = cdiv(p.K, 32);
   const int64_t per = cdiv(nk, kGemvWaves);
@@ -92,7 +74,7 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
   for (int rb = 0; rb < RB; ++rb) wrow[rb] = p.B + min(n0 + 16 * rb + r, p.N - 1) * p.ldb + 8 * g;
   const bool xrow = r < p.M;
   const u16* xp = p.A + (xrow ? r : 0) * p.lda + 8 * g;
-  const float rstd = (XF == 1 && xrow) ? rs[r] : 0.f;
+  float rstd = 0.f;
   f32x4 acc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -109,6 +91,36 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
         w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
+    }
+    if (XF == 1 && j0 == 0) {
+      // RMSNorm row statistics, after the first batch of weight loads is in flight: rmsnorm_fwd_k's
+      // arithmetic (one wave per row, the same summation order), handed over through LDS with a
+      // barrier that waits on the LDS only (the weight loads stay in flight)
+      for (int row = wave; row < p.M; row += kGemvWaves) {
+        const u16* xr = p.A + row * p.lda;
+        float ss = 0.f;
+        for (int c = 0; c * 512 < p.K; ++c) {
+          const int col = c * 512 + lane * 8;
+          if (col < p.K) {
+            const u16x8 xv = *reinterpret_cast<const u16x8*>(xr + col);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += bf2f(xv[j]) * bf2f(xv[j]);
+          }
+        }
+        ss = wave_sum(ss);
+        if (lane == 0) rs[row] = rsqrtf(ss / (float)p.K + a.xf_eps);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      rstd = xrow ? rs[r] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * kGemvWaves + wave;
+      const int64_t kend = ORDER == 0 ? min(nk, (int64_t)(wave + 1) * per) : nk;
+      const int64_t k = ks * 32 + 8 * g;
+      const bool in = j0 + i < per && ks < kend && k < p.K;
+      const int64_t off = in ? ks * 32 : 0;
       x[i] = (in && xrow) ? gemv_xfrag<XF>(a, xp, off, k, rstd) : frag8{};
     }
 #pragma unroll

@@ -24,6 +24,8 @@ from . import ops
 from .functions import StepContext
 from .lora import NO_LORA
 
+FUSE_DECODE_NORMS = False
+
 
 class KVCache:
     """Per-layer K, V [B, Lmax, H*D] in HBM plus the per-row state the decode kernels read."""
@@ -115,9 +117,12 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
     lg = layer.lora_groups
     B = sctx.B
-    # one row per sequence and no adapters: the norms and the SwiGLU run inside the weight-streaming
-    # products (cullavo_decode_linear), bitwise the unfused kernels' values
-    fused = Lnew == 1 and h.shape[0] <= 16 and h.dtype == torch.bfloat16 and all(g is NO_LORA for g in lg.values())
+    # FUSE_DECODE_NORMS: the norms and the SwiGLU inside the weight-streaming products
+    # (cullavo_decode_linear transforms 1 / 2, bitwise the unfused values) -- measured 1.8-2.2x slower
+    # per product than the separate kernels (every workgroup repeats the row transform; 7B step
+    # 7.06 vs 4.05 ms at batch 1, profiles/r04/decode/), so off
+    fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] <= 16 and h.dtype == torch.bfloat16
+             and all(g is NO_LORA for g in lg.values()))
     if fused:
         qkv = ops.decode_linear(h, layer.w_qkv(), transform=1, norm_w=layer.input_layernorm.weight,
                                 eps=cfg.rms_norm_eps)
