@@ -147,40 +147,47 @@ DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int staged, i
   } else {
     smem += staged;  // staged by the last K-tile's iteration, waited for and barriered by the loop
   }
-  // one 16-column group at a time, so only that group's rounded base outputs (TMW x 2 packed
-  // registers) live beside the accumulators: the 288-row tile fits without spilling
+  // one 16-row group at a time: the lora_B fragments (TN x 2) and the bias stay in registers, the
+  // group's rounded base outputs (TN x 2 packed registers) live only while its u B^T is formed, so
+  // the 288-row tile fits the 256 registers without spilling
+  frag8 fb[TN][2];
+  float bv[TN][4];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb[tn][ks] = read_frag<0>(smem + BM2 * BK * 2, wn * WN_COLS + tn * 16, ks, lane);
     const int64_t n = n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[tn][j] = 0.f;
     if (p.bias && n < p.N) {
       const u16x4 b4 = *reinterpret_cast<const u16x4*>(p.bias + n);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = bf2f(b4[j]);
+      for (int j = 0; j < 4; ++j) bv[tn][j] = bf2f(b4[j]);
     }
-    uint32_t base[TMW][2];
+  }
 #pragma unroll
-    for (int tm = 0; tm < TMW; ++tm) {
+  for (int tm = 0; tm < TMW; ++tm) {
+    uint32_t base[TN][2];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
       u16 h[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) h[j] = f2bf(acc[tm][tn][j] * p.alpha + bv[j]);
-      base[tm][0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-      base[tm][1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      for (int j = 0; j < 4; ++j) h[j] = f2bf(acc[tm][tn][j] * p.alpha + bv[tn][j]);
+      base[tn][0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      base[tn][1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
       acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const frag8 fb = read_frag<0>(smem + BM2 * BK * 2, wn * WN_COLS + tn * 16, ks, lane);
+      const frag8 fa = read_frag<0>(smem, wm * (BM2 / 2) + tm * 16, ks, lane);
 #pragma unroll
-      for (int tm = 0; tm < TMW; ++tm) {
-        const frag8 fa = read_frag<0>(smem, wm * (BM2 / 2) + tm * 16, ks, lane);
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc[tm][tn], 0, 0, 0);
-      }
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn][ks], fa, acc[tm][tn], 0, 0, 0);
     }
 #pragma unroll
-    for (int tm = 0; tm < TMW; ++tm) {
-      const float bb[4] = {bf2f((u16)(base[tm][0] & 0xFFFF)), bf2f((u16)(base[tm][0] >> 16)),
-                           bf2f((u16)(base[tm][1] & 0xFFFF)), bf2f((u16)(base[tm][1] >> 16))};
+    for (int tn = 0; tn < TN; ++tn) {
+      const float bb[4] = {bf2f((u16)(base[tn][0] & 0xFFFF)), bf2f((u16)(base[tn][0] >> 16)),
+                           bf2f((u16)(base[tn][1] & 0xFFFF)), bf2f((u16)(base[tn][1] >> 16))};
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[tm][tn][j] = bb[j] + round_bf(acc[tm][tn][j] * p.lora_scale);
     }
