@@ -226,6 +226,34 @@ struct StageDMA {
   }
 };
 
+// StageDMA with one per-lane offset: piece i sits NW * kRP rows (a multiple of 16) below piece 0,
+// where the image swizzle (a function of row & 15) repeats, so its source offset is piece 0's
+// plus a wave-uniform row step, passed as the instruction's scalar offset (inside the buffer's
+// range check like the per-lane part; tests/test_oob_guard.py)
+DEV void lds_dma16s(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned vo, int so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, vo, so, 0, 0);
+}
+template <int ROWS, int D, int NW>
+struct StageDMA1 {
+  static constexpr int kRP = 1024 / (2 * D);
+  static constexpr int kPer = ROWS / kRP / NW;
+  static_assert(kPer * NW * kRP == ROWS && (NW * kRP) % 16 == 0, "pieces must split evenly, 16-row steps");
+  unsigned vo;
+  DEV void prep(int64_t ld, int wave, int lane) {
+    const int r = wave * kRP + lane / (D / 8), s = lane % (D / 8);
+    const int sw = D == 128 ? (((r & 3) << 2) | ((r >> 2) & 3)) : ((r >> 1) & 7);
+    vo = (unsigned)(((int64_t)r * ld + (s ^ sw) * 8) * 2);
+  }
+  DEV void issue(const u16* base, int64_t ld, int row0, int nrows, char* lds, int wave) const {
+    const int left = min(nrows - row0, ROWS);
+    const int bytes = left > 0 ? (int)(((int64_t)(left - 1) * ld + D) * 2) : 0;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * ld), (short)0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) lds_dma16s(rs, lds + (wave + NW * i) * 1024, vo, (int)(i * NW * kRP * ld * 2));
+  }
+};
+
 // row of accumulator register r of a 32x32 tile for lane half h
 DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -360,7 +388,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #define bufK(i) (smem + 2 * (i) * TILE)
 #define bufV(i) (smem + 2 * (i) * TILE + TILE)
   if (t0 < ntiles) {
-    if constexpr (STAGE >= 4) {
+    if constexpr (STAGE == 6) {
+      dma_kv(t0 * KT, 0);
+      dma_kv(t0 * KT, 1);
+    } else if constexpr (STAGE >= 4) {
       dma_kv(t0 * KT, 0);
     } else {
       load_kv(t0 * KT);
@@ -400,7 +431,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
     constexpr int CUR = decltype(cur_c)::value;
     constexpr unsigned PAIR = 2u * CUR * TILE;
     const bool more = t + 1 < ntiles;
-    if constexpr (STAGE >= 4) {
+    if constexpr (STAGE == 6) {
+      // lab only (cullavo_attn_set_stage(6), WRONG results): no K/V loads after the first tile,
+      // every tile computes on the first tile's LDS -- the forward's time without its memory waits
+    } else if constexpr (STAGE >= 4) {
       if (more) dma_kv((t + 1) * KT, CUR ^ 1);  // pair CUR^1 was last read before the previous barrier
     } else {
       if (more) load_kv((t + 1) * KT);
@@ -579,6 +613,363 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = f2bf(o[dt][rr * 4 + j] * inv);
         *reinterpret_cast<u16x4*>(Ob + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+    if (hf == 0) LSE[((int64_t)b * H + h) * Lq + q] = l > 0.f ? (m + log2f(l)) * kLn2 : INFINITY;
+  }
+}
+
+// ============================================================================================
+// forward, software-pipelined (STAGE 7)
+// ============================================================================================
+// attn_fwd_k runs a tile's three steps in order -- S = K Q^T on the matrix pipe, the softmax on
+// the VALU, P V on the matrix pipe -- so inside a wave the matrix pipe idles through the softmax
+// and the VALU through both products. Here iteration t runs tile t's softmax in the issue gaps
+// of tile t+1's S MFMAs (independent work: S_{t+1} does not need tile t's max) and of tile t's
+// first P V MFMAs. K and V have two-slot rings of their own; K runs one tile ahead of V, so at
+// iteration t the K tile t+1 and the V tile t are resident and the DMA of K t+2 / V t+1 lands
+// under the iteration (one barrier per tile, as before). Every LDS read is inline asm with a
+// counted lgkmcnt wait (the fragment group after the current one stays in flight; hipcc puts a
+// vmcnt(0) -- the in-flight LDS-DMA -- in front of the builtin transposed read) and each
+// softmax chunk is pinned beside its MFMA group by sched_group_barrier. Per element the
+// arithmetic is attn_fwd_k's, in the same order: outputs bitwise equal to STAGE 4.
+DEV float swap_max(float x) {
+  // both wave halves' values, max of lane l and lane l ^ 32 (one v_permlane32_swap, no LDS)
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x),
+                                                  false, false);
+  return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+}
+DEV float swap_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x),
+                                                  false, false);
+  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+}
+// NM MFMAs, each followed by NV VALU instructions (the scheduler's placement of the group's code)
+template <int NM, int NV>
+DEV void interleave() {
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (NV > 0) __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+}
+// P = exp2(s c - m) of accumulator registers R0..R0+3 of score tile KT_, the row sum's even /
+// odd partials (the pair order of attn_fwd_k's v_pk_add accumulation)
+// 2 K row fragments (k-steps S0, S0+1 at LDS byte offset OFF from each lane's roff) by inline-asm
+// ds_read_b128, tied by a counted lgkmcnt wait
+template <int NS, int S0, unsigned OFF>
+DEV void k2_issue(s16x8 (&kf)[2], const unsigned (&roff)[NS]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(kf[j]) : "v"(roff[S0 + j]), "n"(OFF) : "memory");
+}
+template <int CNT>
+DEV void k2_tie(s16x8 (&kf)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(kf[0]), "+v"(kf[1]) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int NS, int S0>
+DEV void k2_mfma(const s16x8 (&kf)[2], const frag8 (&qf)[NS], f32x16& acc) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, kf[j]), qf[S0 + j], acc, 0, 0, 0);
+}
+// an empty asm on a value: the code computing it cannot sink below this point, and code reading it
+// cannot rise above it (hipcc's instruction selection otherwise gathers a whole softmax next to its
+// last consumer, out of the MFMA groups it was written beside)
+template <class T>
+DEV void pin(T& x) {
+  asm volatile("" : "+v"(x));
+}
+template <int KT_, int R0>
+DEV void sm_exp4(f32x16 (&sp)[2], float c, float nm, float& rsE, float& rsO) {
+  pin(sp[KT_]);
+#pragma unroll
+  for (int r = R0; r < R0 + 4; r += 2) {
+    const float p0 = fast_exp2(__builtin_fmaf(sp[KT_][r], c, nm));
+    const float p1 = fast_exp2(__builtin_fmaf(sp[KT_][r + 1], c, nm));
+    sp[KT_][r] = p0;
+    sp[KT_][r + 1] = p1;
+    rsE += p0;
+    rsO += p1;
+  }
+  pin(sp[KT_]);
+  pin(rsE);
+  pin(rsO);
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict__ Q, int64_t ldq,
+                                                          const u16* __restrict__ K, int64_t ldk,
+                                                          const u16* __restrict__ V, int64_t ldv,
+                                                          u16* __restrict__ O, int64_t ldo,
+                                                          float* __restrict__ LSE, int H, int Lq, int Lk,
+                                                          float scale, const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 64;
+  constexpr int TILE = KT * D * 2;
+  constexpr int NS = D / 16;  // k-steps over D: 8 (D = 128) or 4 (D = 64)
+  constexpr int ND = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // K slots 0, 1 then V slots 0, 1
+
+  const int nqb = (Lq + 127) / 128;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int q = qb * 128 + wave * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+
+  frag8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    u16x8 v = (q < Lq) ? *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ldq + 16 * s + 8 * hf) : u16x8(0);
+    qf[s] = __builtin_bit_cast(frag8, v);
+  }
+  f32x16 o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) o[i] = f32x16(0.f);
+  float m = -INFINITY, l = 0.f;
+  const float c = scale * kLog2e;
+  const float rescale_thr = g_rescale_thr;
+  const int khi = CAUSAL ? min(Lk, q + 1) : Lk;
+  const unsigned kspan = (unsigned)max(khi - kstart, 0);
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * 128 + 128);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  StageDMA1<KT, D, 4> dk_, dv_;
+  const int w = __builtin_amdgcn_readfirstlane(wave);
+  dk_.prep(ldk, w, lane);
+  dv_.prep(ldv, w, lane);
+  auto dma_k = [&](int t, int slot) { dk_.issue(Kb, ldk, t * KT, Lk, smem + slot * TILE, w); };
+  auto dma_v = [&](int t, int slot) { dv_.issue(Vb, ldv, t * KT, Lk, smem + (2 + slot) * TILE, w); };
+
+  const unsigned sbase = lds_addr(smem);
+  unsigned roff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) roff[s] = sbase + kv_off<D>(lane & 31, 2 * s + hf);
+  unsigned toff[ND][2];
+  {
+    const int i = lane & 15, qq = i >> 2, p = i & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int ch = ((dt * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+      toff[dt][0] = sbase + 2 * TILE + kv_off<D>(4 * hf + qq, ch) + 8 * (p & 1);
+      toff[dt][1] = sbase + 2 * TILE + kv_off<D>(4 * hf + qq + 8, ch) + 8 * (p & 1);
+    }
+  }
+
+  // S = K Q^T of the K tile in slot SLOT, plain (prologue): 4 groups of 4 fragments
+  auto s_plain = [&](auto slot_c, f32x16 (&st)[2]) {
+    constexpr unsigned KO = decltype(slot_c)::value * TILE;
+    s16x8 ka[4], kb[4];
+    st[0] = f32x16(0.f);
+    st[1] = f32x16(0.f);
+    k_group_issue<NS, 0, KO>(ka, roff);
+    k_group_issue<NS, 4, KO>(kb, roff);
+    k_group_tie<4>(ka);
+    k_group_mfma<NS, 0>(ka, qf, st[0]);
+    k_group_issue<NS, 0, KO + 32 * 2 * D>(ka, roff);
+    k_group_tie<4>(kb);
+    k_group_mfma<NS, 4>(kb, qf, st[0]);
+    k_group_issue<NS, 4, KO + 32 * 2 * D>(kb, roff);
+    k_group_tie<4>(ka);
+    k_group_mfma<NS, 0>(ka, qf, st[1]);
+    k_group_tie<0>(kb);
+    k_group_mfma<NS, 4>(kb, qf, st[1]);
+  };
+
+  // one tile: softmax of sp (tile t, scores in registers) beside S of tile t+1 (K slot KS, into
+  // sn; NEXT = false on the last tile: no S), then P V of tile t (V slot VS)
+  auto tile = [&](auto ks_c, auto vs_c, auto next_c, int t, f32x16 (&sp)[2], f32x16 (&sn)[2]) {
+    constexpr unsigned KO = decltype(ks_c)::value * TILE;
+    constexpr unsigned VO = decltype(vs_c)::value * TILE;
+    constexpr bool NEXT = decltype(next_c)::value;
+    if constexpr (NEXT) {
+      // V slot VS^1 was last read by tile t-1's P V, K slot KS^1 by tile t's S (both before the
+      // previous barrier)
+      dma_v(t + 1, decltype(vs_c)::value ^ 1);
+      if (t + 2 < ntiles) dma_k(t + 2, decltype(ks_c)::value ^ 1);
+    }
+    const int kbase = t * KT;
+    const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
+    if (need_mask) {
+      const int koff = kbase + 4 * hf - kstart;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sp[kt][r] = (unsigned)(koff + kt * 32 + acc_row(r, 0)) >= kspan ? -INFINITY : sp[kt][r];
+    }
+    // S of tile t+1 in NS groups of 2 MFMAs (K fragments 2 groups in flight), each group's issue
+    // gaps carrying one (D = 128) or two (D = 64) of the softmax chunks 0-7 of tile t
+    s16x8 ka[2], kb[2];
+    s16x4 lo0[ND], hi0[ND], lo1[ND], hi1[ND];
+    float tmax = -INFINITY, muse = 0.f, alpha = 1.f, rsE = 0.f, rsO = 0.f;
+    bool grow = false;
+    frag8 pf[4];
+    constexpr unsigned K1 = 32 * 2 * D;  // second 32-key half of the K tile
+    constexpr int HG = NS / 2;           // groups per 32-key half
+    // softmax chunk C of tile t and its VALU count (the interleave pattern's filler per MFMA pair)
+    auto chunk = [&](auto c_c) {
+      constexpr int C = decltype(c_c)::value;
+      if constexpr (C == 0) {
+        pin(sp[0]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[0][r]);
+        pin(tmax);
+      } else if constexpr (C == 1) {
+        pin(sp[1]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[1][r]);
+        tmax = swap_max(tmax) * c;
+        grow = __any(tmax > m + rescale_thr);
+        const float mnew = grow ? fmaxf(m, tmax) : m;
+        muse = (mnew == -INFINITY) ? 0.f : mnew;
+        alpha = grow ? fast_exp2(m - muse) : 1.f;
+        l *= alpha;
+        m = mnew;
+        pin(muse);
+        pin(l);
+      } else {
+        constexpr int KT_ = (C - 2) / 4, R0 = ((C - 2) % 4) * 4;
+        sm_exp4<KT_, R0>(sp, c, -muse, rsE, rsO);
+        if constexpr (R0 == 4 || R0 == 12) {
+          pf[2 * KT_ + R0 / 8] = pack_frag(sp[KT_], R0 / 8);
+          pin(pf[2 * KT_ + R0 / 8]);
+        }
+      }
+    };
+    constexpr int kFill[8] = {4, 6, 6, 8, 6, 8, 6, 8};
+    // group G: its MFMAs, its chunk(s), then the reads two groups ahead (or the first P V reads)
+    auto group = [&](auto g_c) {
+      constexpr int G = decltype(g_c)::value;
+      constexpr unsigned OFF = KO + (G / HG) * K1;
+      constexpr int S0 = 2 * (G % HG);
+      if constexpr (NEXT) {
+        if constexpr (G % 2 == 0) {
+          k2_tie<G == NS - 1 ? 2 * ND : 2>(ka);
+          k2_mfma<NS, S0>(ka, qf, sn[G / HG]);
+        } else {
+          k2_tie<G == NS - 1 ? 2 * ND : 2>(kb);
+          k2_mfma<NS, S0>(kb, qf, sn[G / HG]);
+        }
+      }
+      constexpr int CPG = 8 / NS;  // chunks per group
+      chunk(std::integral_constant<int, G * CPG>{});
+      if constexpr (CPG == 2) chunk(std::integral_constant<int, G * CPG + 1>{});
+      if constexpr (NEXT) interleave<2, kFill[G * CPG] + (CPG == 2 ? kFill[G * CPG + 1] : 0)>();
+      if constexpr (G + 2 < NS) {
+        if constexpr (NEXT) {
+          constexpr unsigned OFF2 = KO + ((G + 2) / HG) * K1;
+          if constexpr (G % 2 == 0) k2_issue<NS, 2 * ((G + 2) % HG), OFF2>(ka, roff);
+          else k2_issue<NS, 2 * ((G + 2) % HG), OFF2>(kb, roff);
+        }
+      } else if constexpr (G == NS - 2) {
+        tr_group_issue<ND, VO + 0 * 2 * D>(lo0, hi0, toff);
+      } else {
+        tr_group_issue<ND, VO + 16 * 2 * D>(lo1, hi1, toff);
+      }
+      (void)OFF;
+    };
+    if constexpr (NEXT) {
+      sn[0] = f32x16(0.f);
+      sn[1] = f32x16(0.f);
+      k2_issue<NS, 0, KO>(ka, roff);
+      k2_issue<NS, 2 * (1 % HG), KO + (1 / HG) * K1>(kb, roff);
+    }
+    group(std::integral_constant<int, 0>{});
+    group(std::integral_constant<int, 1>{});
+    group(std::integral_constant<int, 2>{});
+    group(std::integral_constant<int, 3>{});
+    if constexpr (NS == 8) {
+      group(std::integral_constant<int, 4>{});
+      group(std::integral_constant<int, 5>{});
+      group(std::integral_constant<int, 6>{});
+      group(std::integral_constant<int, 7>{});
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (grow) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) o[i] *= alpha;
+    }
+    // P V, slice 0 | P of registers 8-15 of score tile 1
+    tr_group_tie<ND, 2 * ND>(lo0, hi0);
+    tr_group_mfma<ND>(lo0, hi0, pf[0], o);
+    sm_exp4<1, 8>(sp, c, -muse, rsE, rsO);
+    sm_exp4<1, 12>(sp, c, -muse, rsE, rsO);
+    pf[3] = pack_frag(sp[1], 1);
+    pin(pf[3]);
+    interleave<ND, 7>();
+    tr_group_issue<ND, VO + 32 * 2 * D>(lo0, hi0, toff);
+    // slice 1 | the row sum
+    tr_group_tie<ND, 2 * ND>(lo1, hi1);
+    tr_group_mfma<ND>(lo1, hi1, pf[1], o);
+    {
+      float rs = rsE + rsO;
+      rs = swap_sum(rs);
+      l += rs;
+    }
+    interleave<ND, 1>();
+    tr_group_issue<ND, VO + 48 * 2 * D>(lo1, hi1, toff);
+    tr_group_tie<ND, 2 * ND>(lo0, hi0);
+    tr_group_mfma<ND>(lo0, hi0, pf[2], o);
+    tr_group_tie<ND, 0>(lo1, hi1);
+    tr_group_mfma<ND>(lo1, hi1, pf[3], o);
+    if constexpr (NEXT) {
+      // K t+2 / V t+1 landed (vmcnt counts LDS-DMA), and every wave's reads of the slots they
+      // refill next iteration are done
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+
+  f32x16 sa[2], sb[2];
+  if (t0 < ntiles) {
+    dma_k(t0, 0);
+    dma_v(t0, 0);
+    if (t0 + 1 < ntiles) dma_k(t0 + 1, 1);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    __syncthreads();
+    s_plain(std::integral_constant<int, 0>{}, sa);
+    __syncthreads();  // K slot 0 is refilled (tile t0 + 2) by the first iteration
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using NT = std::integral_constant<bool, true>;
+    using NF = std::integral_constant<bool, false>;
+    // tile t: K slot of tile t+1 = (t - t0 + 1) & 1, V slot of tile t = (t - t0) & 1. Pairs of
+    // tiles with a successor in a plain loop, the last one or two after it (a loop with the last
+    // tile's variant inside it spilled ~95 VGPRs)
+    int t = t0;
+    for (; t + 2 < ntiles; t += 2) {
+      tile(I1{}, I0{}, NT{}, t, sa, sb);
+      tile(I0{}, I1{}, NT{}, t + 1, sb, sa);
+    }
+    if (t + 1 < ntiles) {
+      tile(I1{}, I0{}, NT{}, t, sa, sb);
+      tile(I0{}, I1{}, NF{}, t + 1, sb, sa);
+    } else {
+      tile(I1{}, I0{}, NF{}, t, sa, sb);
+    }
+  }
+
+  if (q < Lq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    u16* Ob = O + ((int64_t)b * Lq + q) * ldo + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 wv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = f2bf(o[dt][rr * 4 + j] * inv);
+        *reinterpret_cast<u16x4*>(Ob + dt * 32 + 8 * rr + 4 * hf) = wv;
       }
     if (hf == 0) LSE[((int64_t)b * H + h) * Lq + q] = l > 0.f ? (m + log2f(l)) * kLn2 : INFINITY;
   }
@@ -1593,10 +1984,16 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
     set_smem(attn_fwd_k<D, CAUSAL, 2, 1>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 4>, smem);
     set_smem(attn_fwd_k<D, CAUSAL, 5>, smem);
+    set_smem(attn_fwd_k<D, CAUSAL, 6>, smem);
+    set_smem(attn_fwd_pipe_k<D, CAUSAL>, smem);
     once = true;
   }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  if (g_fwd_stage == 5)
+  if (g_fwd_stage == 7)
+    attn_fwd_pipe_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 6)
+    attn_fwd_k<D, CAUSAL, 6><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
+  else if (g_fwd_stage == 5)
     attn_fwd_k<D, CAUSAL, 5><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   else if (g_fwd_stage == 4)
     attn_fwd_k<D, CAUSAL, 4><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
@@ -1738,7 +2135,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int prev = g_fwd_stage;
-  if (buffer_loads >= 0 && buffer_loads <= 5) g_fwd_stage = buffer_loads;
+  if (buffer_loads >= 0 && buffer_loads <= 7) g_fwd_stage = buffer_loads;
   return prev;
 }
 

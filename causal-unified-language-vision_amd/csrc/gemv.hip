@@ -58,8 +58,11 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, f
 // (at any moment a workgroup reads one contiguous 512-B run per weight row); RB: 16-row blocks per
 // workgroup (each wave computes all of them over its k-steps). Measured alike on the 7B decode
 // step (ORDER 0 / 1: 4.14 / 4.16 ms per token; RB 2: 4.66-4.79, profiles/r04/decode/).
-template <int CT, int ORDER, int RB, int XF>
-__global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
+// NBW: W fragment loads per batch and wave. 16 keeps 151 VGPRs (one workgroup per CU: every
+// workgroup's load ramp and reduction are exposed); 8 fits 2 workgroups per CU (86 VGPRs) and
+// 4 fits 4, so one workgroup's ramp / reduction runs under the others' streams.
+template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : NBW >= 8 ? 4 : 8))) void gemv_k(GemvArgs a) {
   const GemmArgs& p = a.g;
   __shared__ f32x4 red[kGemvWaves][RB][64];
   __shared__ float rs[16];
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
   f32x4 acc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int NB = kGemvBatch / RB;  // k-steps per batch (W loads per batch stay kGemvBatch)
+  constexpr int NB = NBW / RB;  // k-steps per batch (W loads per batch stay NBW)
   for (int64_t j0 = 0; j0 < per; j0 += NB) {
     frag8 w[NB][RB], x[NB];
 #pragma unroll
@@ -143,16 +146,19 @@ __global__ __launch_bounds__(512, 1) void gemv_k(GemvArgs a) {
 
 int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   // lab switch (CULLAVO_GEMV: 0 contiguous K ranges, 1 round-robin k-steps, 2 / 3 = 0 / 1 with
-  // 32 rows per workgroup), read once per process
+  // 32 rows per workgroup, 4 / 5 = 0 / 1 with 8-load batches at 2 workgroups per CU, 6 / 7 = 0 / 1
+  // with 4-load batches at 4 workgroups per CU), read once per process
   static const int v = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : kGemvDefault;
-  const int rb = (v & 2) ? 2 : 1;
+  const int rb = (v == 2 || v == 3) ? 2 : 1;
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
   GemvArgs a{};
   a.g = p;
-#define GV(O, R)                                                                                      \
-  if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);                         \
-  else gemv_k<CULLAVO_DT_BF16, O, R, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  if (v == 0) { GV(0, 1) } else if (v == 1) { GV(1, 1) } else if (v == 2) { GV(0, 2) } else { GV(1, 2) }
+#define GV(O, R, NBW)                                                                                 \
+  if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);                    \
+  else gemv_k<CULLAVO_DT_BF16, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  if (v == 0) { GV(0, 1, 16) } else if (v == 1) { GV(1, 1, 16) } else if (v == 2) { GV(0, 2, 16) }
+  else if (v == 3) { GV(1, 2, 16) } else if (v == 4) { GV(0, 1, 8) } else if (v == 5) { GV(1, 1, 8) }
+  else if (v == 6) { GV(0, 1, 4) } else { GV(1, 1, 4) }
 #undef GV
   return cullavo_check_launch("gemv");
 }

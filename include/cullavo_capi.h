@@ -144,7 +144,11 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
  * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
  * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers), 10 = 288x256 /
  * 8 waves (falls back to 2 when A is not K-contiguous; chosen automatically only for K >= 2048),
- * 11 = mode 10 with the other loader-wave choice (A/B testing).
+ * 11 = mode 10 with the other loader-wave choice (A/B testing), 12 / 13 = the 256x256
+ * ping-pong wave-group kernel (two 4-wave groups alternating MFMA and LDS-DMA phases; 4 / 5
+ * LDS stages, 16x16x32 MFMAs), 15 / 16 = modes 12 / 13 with 32x32x16 MFMAs (all four measured
+ * slower than modes 2 / 10 on the 7B step shapes, profiles/r04/gemm/; never chosen
+ * automatically; need a_layout = b_layout = 0).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
@@ -192,7 +196,9 @@ int cullavo_gemm_set_loaders(int mode);
  * 9 = the 8-wave 256x256 kernel split over K (a grid of at most half the CUs with >= 32
  * K-tiles, both M and N >= 256): used by cullavo_gemm_ex when the caller passes the workspace
  * cullavo_gemm_workspace() asks for; f32 partials [splits][M][N], reduced in split order
- * (deterministic) with the full epilogue. cullavo_gemm itself (no workspace) never splits. */
+ * (deterministic) with the full epilogue. cullavo_gemm itself (no workspace) never splits.
+ * 14 = the weight-streaming decode product (gemv.hip: M <= 16 rows, a_layout = b_layout = 0,
+ * automatic tile mode, no dropout): one 8-wave workgroup per 16 rows of B, no workspace. */
 int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid);
 
 /* ---- norms -------------------------------------------------------------------------------

@@ -631,7 +631,8 @@ def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
     """The forward's K/V staging variants (cullavo_attn_set_stage: 2 = per-tile scalar descriptor;
     1 = per-chunk range-checked buffer loads; 0 = pointer loads; 3 = 2 with raised
     MFMA priority; 4 = LDS-DMA straight into the swizzled image, the default; 5 = 4 with inline-asm fragment
-    reads in counted groups) stage the same bytes
+    reads in counted groups; 7 = the software-pipelined D = 128 kernel, softmax of tile t beside
+    the S MFMAs of tile t+1) stage the same bytes
     (rows past the sequence end as zeros), so O and LSE are bitwise equal: ragged last tiles
     (L % 64 != 0), a partial single tile (L = 33), left-padded rows (kv_start), the LM D = 128
     causal and ViT D = 64 shapes; and the default matches the float reference."""
@@ -645,12 +646,12 @@ def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
     outs = {}
     prev = L_.cullavo_attn_set_stage(2)
     try:
-        for mode in (2, 1, 0, 3, 4, 5):
-            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2, 3, 4, 5)
+        for mode in (2, 1, 0, 3, 4, 5, 7):
+            assert L_.cullavo_attn_set_stage(mode) in (0, 1, 2, 3, 4, 5, 7)
             outs[mode] = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
     finally:
         L_.cullavo_attn_set_stage(prev)
-    for mode in (1, 0, 3, 4, 5):
+    for mode in (1, 0, 3, 4, 5, 7):
         assert torch.equal(outs[2][0], outs[mode][0]), f"O differs, stage {mode}"
         assert torch.equal(outs[2][1], outs[mode][1]), f"LSE differs, stage {mode}"
     if ks is None:
@@ -1067,3 +1068,35 @@ def test_gemm_l2_prefetch_bitwise(tile, al, bl, M, N, K):
     if M * N * K <= 2 ** 31:
         z = (A.float().T if al else A.float()) @ (B.float() if bl else B.float().T)
         close(outs[0], z + (bias.float() if bias is not None else 0), 8e-3, f"prefetch {M}x{N}x{K}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thr", [0.0, 8.0])
+def test_attention_fwd_pipelined_rescale_bitwise(thr):
+    """The pipelined forward (stage 7) takes the deferred-rescale branch at the same tiles as stage 4
+    and rescales O and l and nothing else: bitwise equal O / LSE at threshold 0 (rescale at every
+    max growth) and 8, on a spike key in the 4th tile that moves every later row's max (the
+    construction of test_attention_rescale_threshold) and a ragged causal length."""
+    from cullavo_amd import _lib
+    B, H, L, D = 2, 2, 1000, 128
+    u = rnd((1, 1, H, D), 78).float()
+    q = (rnd((B, L, H, D), 75).float() + u).reshape(B * L, H * D).to(BF)
+    kh = rnd((B, L, H, D), 76).float()
+    v = rnd((B * L, H * D), 77)
+    kh[:, 230] = 3.0 * u[0, 0]
+    kh[:, 700] = 3.5 * u[0, 0]
+    k = kh.reshape(B * L, H * D).to(BF)
+    kw = dict(B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=True)
+    L_ = _lib.lib()
+    prev = L_.cullavo_attn_set_stage(4)
+    try:
+        assert L_.cullavo_attn_set_rescale(ctypes.c_float(thr), None) == 0
+        o4, lse4 = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
+        L_.cullavo_attn_set_stage(7)
+        o7, lse7 = ops().attn_fwd(q.to(DEV), k.to(DEV), v.to(DEV), **kw)
+    finally:
+        L_.cullavo_attn_set_stage(prev)
+        L_.cullavo_attn_set_rescale(ctypes.c_float(8.0), None)
+    assert torch.equal(o4, o7) and torch.equal(lse4, lse7)
+    _, _, _, o_ref = _attn_ref(q, k, v, B, H, L, D, True)
+    close(o7, o_ref.transpose(1, 2).reshape(B * L, H * D), 1.2e-2, "attn o (stage 7)")
