@@ -800,11 +800,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
     if (need_mask) {
       const int koff = kbase + 4 * hf - kstart;
+      if (kbase >= kstart) {
+        // koff >= 0: key j of the tile is live iff j < kspan - koff (one compare against a
+        // constant per score instead of an add and an unsigned compare)
+        const int lim = (int)kspan - koff;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          sp[kt][r] = (unsigned)(koff + kt * 32 + acc_row(r, 0)) >= kspan ? -INFINITY : sp[kt][r];
+          for (int r = 0; r < 16; ++r) sp[kt][r] = kt * 32 + acc_row(r, 0) < lim ? sp[kt][r] : -INFINITY;
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            sp[kt][r] = (unsigned)(koff + kt * 32 + acc_row(r, 0)) >= kspan ? -INFINITY : sp[kt][r];
+      }
     }
     // S of tile t+1 in NS groups of 2 MFMAs (K fragments 2 groups in flight), each group's issue
     // gaps carrying one (D = 128) or two (D = 64) of the softmax chunks 0-7 of tile t
@@ -1838,6 +1848,358 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w64_k(
 }
 
 // ============================================================================================
+// backward dK/dV, software-pipelined (mode 8)
+// ============================================================================================
+// One wave per SIMD: 4 waves, 128 keys per workgroup, each wave's 32 keys held as K and V row
+// fragments in registers (512 registers per wave leave room for them, for the 128 dK/dV
+// accumulators and for two tiles' S/dP), the workgroup sweeping 32-query Q / dO tiles through a
+// 3-slot LDS ring filled by LDS-DMA two tiles ahead (lse and delta ride along, 4 B per lane). Per
+// tile and wave (32 keys x 32 queries): S = Q K^T, dP = dO V^T (16 MFMAs), P = exp2(S c - lse),
+// dS = P (dP - delta) (VALU), dV += P^T dO, dK += dS^T Q (16 MFMAs). Iteration t runs tile t's
+// elementwise step in the issue gaps of tile t+1's S / dP MFMAs, then tile t's dV / dK MFMAs;
+// every LDS read is inline asm in counted groups (the next group in flight under the current
+// MFMAs). The elementwise arithmetic and the dS^T written for the dQ kernel are attn_bwd_dkdv8_k's
+// (bitwise); dK / dV sum a key's queries in sweep order (mode 7 adds two half-tile partials).
+template <int NR, unsigned OFF>
+DEV void rd128(s16x8 (&f)[NR], const unsigned (&a)[NR]) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[j]) : "v"(a[j]), "n"(OFF) : "memory");
+}
+template <int CNT, int NR>
+DEV void tie128(s16x8 (&f)[NR]) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[j]) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <unsigned OFF>
+DEV void rdtr(s16x4& lo, s16x4& hi, unsigned alo, unsigned ahi) {
+  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+               : "=&v"(lo), "=&v"(hi) : "v"(alo), "v"(ahi), "n"(OFF) : "memory");
+}
+template <int CNT>
+DEV void tietr(s16x4& a, s16x4& b, s16x4& c, s16x4& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+DEV frag8 cat_tr(const s16x4& lo, const s16x4& hi) {
+  return __builtin_bit_cast(frag8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+DEV void lds_dma4(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned vo) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 4, vo, 0, 0, 0);
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_k(
+    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
+    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
+    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
+    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
+    const int32_t* __restrict__ kv_start, u16* __restrict__ dST, int64_t ldst, int64_t st_bh) {
+  constexpr int QT = 32, KB = 128;
+  constexpr int TQ = QT * D * 2;      // bytes of a Q (or dO) tile image
+  constexpr int SLOT = 2 * TQ + 512;  // [Q | dO | lse(32, 256-B area) | delta(32, 256-B area)]
+  constexpr int NS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int NG = NS / 2;          // S / dP groups: 2 k-steps = 4 MFMAs each
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nkb = (Lk + KB - 1) / KB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = lid % nkb, hb = lid / nkb;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int k0 = kb * KB + 32 * wave;
+  const int key = k0 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+  const int qlo = CAUSAL ? key : 0;
+  const int qlim = (key < kstart || key >= Lk) ? qlo : Lq;
+  const unsigned qspan = (unsigned)max(qlim - qlo, 0);
+
+  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
+  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
+  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
+  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
+
+  frag8 kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const bool in = key < Lk;
+    kf[s] = __builtin_bit_cast(frag8, in ? *reinterpret_cast<const u16x8*>(Kb + (int64_t)key * ldk + 16 * s + 8 * hf) : u16x8(0));
+    vf[s] = __builtin_bit_cast(frag8, in ? *reinterpret_cast<const u16x8*>(Vb + (int64_t)key * ldv + 16 * s + 8 * hf) : u16x8(0));
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dk[i] = f32x16(0.f); dv[i] = f32x16(0.f); }
+  const float c = scale * kLog2e;
+  const int kmin = kb * KB;
+  const int qt0 = CAUSAL ? (kmin / QT) : 0;
+  const int nqt = (Lq + QT - 1) / QT;
+  const bool block_live = kmin < Lk && (kmin + KB > kstart);
+
+  StageDMA1<QT, D, 4> dq_, ddo_;
+  dq_.prep(ldq, wave, lane);
+  ddo_.prep(lddo, wave, lane);
+  // tile t into slot sl: Q, dO images (every wave its pieces), lse / delta (wave 0, one 4-byte
+  // LDS-DMA each by waves 0 / 1; rows past Lq land as zeros and are masked)
+  auto dma = [&](int t, int sl) {
+    char* base = smem + sl * SLOT;
+    dq_.issue(Qb, ldq, t * QT, Lq, base, wave);
+    ddo_.issue(dOb, lddo, t * QT, Lq, base + TQ, wave);
+    if (wave < 2) {
+      // lse (wave 0) / delta (wave 1): 64 lanes x 4 B into a 256-B area each, rows past the tile
+      // or Lq outside the descriptor's range (zeros)
+      const int left = min(Lq - t * QT, QT);
+      const int bytes = left > 0 ? left * 4 : 0;
+      const float* src = (wave == 0 ? lseb : delb) + t * QT;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, bytes, 0x00020000);
+      lds_dma4(rs, base + 2 * TQ + 256 * wave, (unsigned)(lane * 4));
+    }
+  };
+
+  // per-lane LDS byte offsets within a slot: Q / dO row fragments (A operands of S / dP; dO at
+  // +TQ), their transposed fragments (B operands of dV / dK, 16-query half s at +16 s rows), and
+  // this lane's four lse / delta quads (query rows 8 rr + 4 hf + 0..3)
+  const unsigned sbase = lds_addr(smem);
+  unsigned roff[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) roff[s] = kv_off<D>(lane & 31, 2 * s + hf);
+  unsigned toff[ND][2];
+  {
+    const int i = lane & 15, qq = i >> 2, p = i & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int ch = ((dt * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+      toff[dt][0] = kv_off<D>(4 * hf + qq, ch) + 8 * (p & 1);
+      toff[dt][1] = kv_off<D>(4 * hf + qq + 8, ch) + 8 * (p & 1);
+    }
+  }
+  const unsigned laux = 2 * TQ + 16 * hf;  // + 32 rr bytes; delta at + 256
+
+  u16* dsrow = dST + ((int64_t)b * H + h) * st_bh + (int64_t)key * ldst + 4 * hf;
+
+  // S / dP of the tile in slot base sb (bytes), plain (prologue)
+  auto sdp_plain = [&](unsigned sb, f32x16& sa, f32x16& pa) {
+    sa = f32x16(0.f);
+    pa = f32x16(0.f);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(sbase + sb + roff[s]), kf[s], sa, 0, 0, 0);
+      pa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(sbase + sb + TQ + roff[s]), vf[s], pa, 0, 0, 0);
+    }
+  };
+
+  // iteration t: sc / pc hold tile t's S / dP (slot base cb); NEXT: tile t+1's S / dP (slot nb)
+  // into sn / pn beside tile t's elementwise step; then tile t's dV / dK
+  auto iter = [&](auto next_c, int t, unsigned cb, unsigned nb, f32x16& sc, f32x16& pc, f32x16& sn, f32x16& pn) {
+    constexpr bool NEXT = decltype(next_c)::value;
+    // mask (tiles crossing the causal diagonal of this wave's keys, the sequence end, kv_start)
+    const bool need_mask = (CAUSAL && t * QT < k0 + 32) || t * QT + QT > Lq || k0 < kstart || k0 + 32 > Lk;
+    if (need_mask) {
+      const int qoff = t * QT + 4 * hf - qlo;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        sc[r] = (unsigned)(qoff + acc_row(r, 0)) >= qspan ? -INFINITY : sc[r];
+    }
+    // lse / delta quads of tile t (issued first: the first group's counted wait covers them)
+    s16x8 aux[8];
+    {
+      unsigned aa[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) aa[j] = sbase + cb + laux + 32 * (j & 3) + 256 * (j >> 2);
+      rd128<8, 0>(aux, aa);
+    }
+    s16x8 ga[4], gb[4];
+    auto issue = [&](auto g_c, s16x8 (&f)[4]) {
+      constexpr int G = decltype(g_c)::value;
+      unsigned a[4] = {sbase + nb + roff[2 * G], sbase + nb + roff[2 * G], sbase + nb + roff[2 * G + 1],
+                       sbase + nb + roff[2 * G + 1]};
+      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[0]) : "v"(a[0]) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[1]) : "v"(a[1]), "n"(TQ) : "memory");
+      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[2]) : "v"(a[2]) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[3]) : "v"(a[3]), "n"(TQ) : "memory");
+    };
+    auto mm = [&](auto g_c, s16x8 (&f)[4]) {
+      constexpr int G = decltype(g_c)::value;
+      sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[0]), kf[2 * G], sn, 0, 0, 0);
+      pn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[1]), vf[2 * G], pn, 0, 0, 0);
+      sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[2]), kf[2 * G + 1], sn, 0, 0, 0);
+      pn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[3]), vf[2 * G + 1], pn, 0, 0, 0);
+    };
+    frag8 pf[2], df[2];
+    // elementwise chunk rr: accumulator registers 4 rr .. 4 rr + 3 (query rows 8 rr + 4 hf + 0..3)
+    auto chunk = [&](auto rr_c) {
+      constexpr int RR = decltype(rr_c)::value;
+      // the quads are valid only after the group's counted wait: every use stays below these pins
+      // (no pins on the S / dP accumulators: an asm operand would move them out of AGPRs)
+      pin(aux[RR]);
+      pin(aux[4 + RR]);
+      const f32x4 l4 = __builtin_bit_cast(f32x4, aux[RR]);
+      const f32x4 d4 = __builtin_bit_cast(f32x4, aux[4 + RR]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = RR * 4 + j;
+        const float pv = fast_exp2(fmaf(sc[r], c, -(l4[j] * kLog2e)));
+        sc[r] = pv;
+        pc[r] = pv * (pc[r] - d4[j]);
+      }
+      if constexpr (RR % 2 == 1) {
+        constexpr int S = RR / 2;
+        pf[S] = pack_frag(sc, S);
+        df[S] = pack_frag(pc, S);
+        const u16x8 w = __builtin_bit_cast(u16x8, df[S]);
+        u16* row = dsrow + t * QT + 16 * S;
+        *reinterpret_cast<u16x4*>(row) = u16x4{w[0], w[1], w[2], w[3]};
+        *reinterpret_cast<u16x4*>(row + 8) = u16x4{w[4], w[5], w[6], w[7]};
+        pin(pf[S]);
+        pin(df[S]);
+      }
+    };
+    if constexpr (NEXT) {
+      sn = f32x16(0.f);
+      pn = f32x16(0.f);
+      issue(std::integral_constant<int, 0>{}, ga);
+      issue(std::integral_constant<int, 1>{}, gb);
+      // group 0
+      tie128<4, 4>(ga);
+      mm(std::integral_constant<int, 0>{}, ga);
+      chunk(std::integral_constant<int, 0>{});
+      interleave<4, 5>();
+      if constexpr (NG > 2) issue(std::integral_constant<int, 2 % NG>{}, ga);
+      // group 1
+      tie128<(NG > 2 ? 4 : 0), 4>(gb);
+      mm(std::integral_constant<int, 1>{}, gb);
+      chunk(std::integral_constant<int, 1>{});
+      interleave<4, 9>();
+      if constexpr (NG > 2) {
+        issue(std::integral_constant<int, 3 % NG>{}, gb);
+        // groups 2, 3
+        tie128<4, 4>(ga);
+        mm(std::integral_constant<int, 2 % NG>{}, ga);
+        chunk(std::integral_constant<int, 2>{});
+        interleave<4, 5>();
+        tie128<0, 4>(gb);
+        mm(std::integral_constant<int, 3 % NG>{}, gb);
+        chunk(std::integral_constant<int, 3>{});
+        interleave<4, 9>();
+      } else {
+        chunk(std::integral_constant<int, 2>{});
+        chunk(std::integral_constant<int, 3>{});
+      }
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      chunk(std::integral_constant<int, 0>{});
+      chunk(std::integral_constant<int, 1>{});
+      chunk(std::integral_constant<int, 2>{});
+      chunk(std::integral_constant<int, 3>{});
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // dV += P^T dO, dK += dS^T Q over tile t (slot cb): per (half s, column block dt) the dO and Q
+    // transposed fragments (4 tr reads), one group ahead
+    s16x4 ta[4], tb[4];
+    auto tiss = [&](auto i_c, s16x4 (&f)[4]) {
+      constexpr int I = decltype(i_c)::value;
+      constexpr int S = I / ND, DT = I % ND;
+      constexpr unsigned RO = 16 * S * 2 * D;
+      rdtr<TQ + RO>(f[0], f[1], sbase + cb + toff[DT][0], sbase + cb + toff[DT][1]);
+      rdtr<RO>(f[2], f[3], sbase + cb + toff[DT][0], sbase + cb + toff[DT][1]);
+    };
+    auto tmm = [&](auto i_c, s16x4 (&f)[4]) {
+      constexpr int I = decltype(i_c)::value;
+      constexpr int S = I / ND, DT = I % ND;
+      dv[DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[S], cat_tr(f[0], f[1]), dv[DT], 0, 0, 0);
+      dk[DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df[S], cat_tr(f[2], f[3]), dk[DT], 0, 0, 0);
+    };
+    constexpr int NI = 2 * ND;
+    tiss(std::integral_constant<int, 0>{}, ta);
+    tiss(std::integral_constant<int, 1>{}, tb);
+    auto tstep = [&](auto i_c) {
+      constexpr int I = decltype(i_c)::value;
+      if constexpr (I % 2 == 0) {
+        tietr<I + 1 < NI ? 4 : 0>(ta[0], ta[1], ta[2], ta[3]);
+        tmm(i_c, ta);
+        if constexpr (I + 2 < NI) tiss(std::integral_constant<int, I + 2>{}, ta);
+      } else {
+        tietr<I + 1 < NI ? 4 : 0>(tb[0], tb[1], tb[2], tb[3]);
+        tmm(i_c, tb);
+        if constexpr (I + 2 < NI) tiss(std::integral_constant<int, I + 2>{}, tb);
+      }
+    };
+    tstep(std::integral_constant<int, 0>{});
+    tstep(std::integral_constant<int, 1>{});
+    tstep(std::integral_constant<int, 2>{});
+    tstep(std::integral_constant<int, 3>{});
+    if constexpr (NI > 4) {
+      tstep(std::integral_constant<int, 4 % NI>{});
+      tstep(std::integral_constant<int, 5 % NI>{});
+      tstep(std::integral_constant<int, 6 % NI>{});
+      tstep(std::integral_constant<int, 7 % NI>{});
+    }
+    if constexpr (NEXT) {
+      // tile t+2 landed; every wave's reads of slot cb (refilled next iteration) are done
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+
+  if (block_live && qt0 < nqt) {
+    dma(qt0, 0);
+    if (qt0 + 1 < nqt) dma(qt0 + 1, 1);
+    __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    __syncthreads();
+    f32x16 sa, pa, sb2, pb2;
+    sdp_plain(0, sa, pa);
+    using NT = std::integral_constant<bool, true>;
+    using NF = std::integral_constant<bool, false>;
+    // slots rotate 0 -> 1 -> 2; iteration t refills slot (t - qt0 + 2) % 3 with tile t + 2
+    int t = qt0;
+    unsigned cs = 0, ns = 1;  // slot of tile t, of tile t + 1
+    auto step = [&](auto next_c, f32x16& sc, f32x16& pc, f32x16& sn, f32x16& pn) {
+      const unsigned fs = 3 - cs - ns;  // the third slot
+      if constexpr (decltype(next_c)::value) {
+        if (t + 2 < nqt) dma(t + 2, (int)fs);
+      }
+      iter(next_c, t, cs * SLOT, ns * SLOT, sc, pc, sn, pn);
+      cs = ns;
+      ns = fs;
+      ++t;
+    };
+    for (; t + 2 < nqt;) {
+      step(NT{}, sa, pa, sb2, pb2);
+      step(NT{}, sb2, pb2, sa, pa);
+    }
+    if (t + 1 < nqt) {
+      step(NT{}, sa, pa, sb2, pb2);
+      step(NF{}, sb2, pb2, sa, pa);
+    } else {
+      step(NF{}, sa, pa, sb2, pb2);
+    }
+  }
+
+  // dK (x scale) and dV of this wave's 32 keys: lane column d = 32 dt + (lane & 31), rows
+  // acc_row(r, hf) (scalar row offsets, one 32-bit lane offset, as attn_bwd_dkdv8_k)
+  u16* dKr = dK + ((int64_t)b * Lk + k0) * lddk + (int64_t)h * D;
+  u16* dVr = dV + ((int64_t)b * Lk + k0) * lddv + (int64_t)h * D;
+  const unsigned lk = (unsigned)(4 * hf * lddk + (lane & 31)) * 2u, lv = (unsigned)(4 * hf * lddv + (lane & 31)) * 2u;
+  const int left = Lk - k0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (acc_row(r, hf) < left) {
+      u16* pk = dKr + (int64_t)acc_row(r, 0) * lddk;
+      u16* pv = dVr + (int64_t)acc_row(r, 0) * lddv;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        *(u16*)((char*)pk + (lk + dt * 64u)) = f2bf(dk[dt][r] * scale);
+        *(u16*)((char*)pv + (lv + dt * 64u)) = f2bf(dv[dt][r]);
+      }
+    }
+  }
+}
+
+// ============================================================================================
 // backward dQ from the stored dS (mode 7)
 // ============================================================================================
 // The 8-wave dK/dV kernel writes dS^T[b, h][key][q] (bf16, the same rounded values its dK
@@ -2073,10 +2435,11 @@ template <int D, bool CAUSAL>
 int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
                   int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
                   u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
-                  const int32_t* ks, u16* ds, hipStream_t s) {
+                  const int32_t* ks, u16* ds, hipStream_t s, bool pipe = false) {
   const int64_t rows = (int64_t)B * Lq * H;
   attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
+  const int smem_p = 3 * (2 * 32 * D * 2 + 512);
   const int smem_b = 2 * (64 * D * 2 + 64 * 128 * 2);
   static bool once = false;
   if (!once) {
@@ -2084,10 +2447,14 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true, true>, smem_a);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL, true>, smem_b);
+    set_smem(attn_bwd_dkdv_pipe_k<D, CAUSAL>, smem_p);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
-  if (g_bwd_stage & 1)
+  if (pipe)
+    attn_bwd_dkdv_pipe_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 256, smem_p, s>>>(
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
+  else if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, true, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
   else
@@ -2155,7 +2522,7 @@ extern "C" int cullavo_attn_set_rescale(float threshold, float* previous) {
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
   const int prev = g_bwd_tiles;
-  if (mode >= -1 && mode <= 7) g_bwd_tiles = mode;
+  if (mode >= -1 && mode <= 8) g_bwd_tiles = mode;
   return prev;
 }
 
@@ -2188,7 +2555,8 @@ extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64
 static int bwd_mode(int D) { return g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 7 : 2); }
 
 extern "C" size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype) {
-  if (dtype != CULLAVO_DT_BF16 || D < 64 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || bwd_mode(D) != 7) return 0;
+  if (dtype != CULLAVO_DT_BF16 || D < 64 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (bwd_mode(D) != 7 && bwd_mode(D) != 8))
+    return 0;
   return (size_t)B * H * ds_rows(Lk) * ds_cols(Lq) * 2;
 }
 
@@ -2229,10 +2597,11 @@ extern "C" int cullavo_attn_bwd_ws(const void* q, int64_t ldq, const void* k, in
   // B=64, T=577, H=16): there the 4-wave kernels already hold K/V in registers at < 256
   // VGPRs and the 8-wave LDS re-reads cost more than the second wave hides (tools/attn_bench.py)
   int mode = bwd_mode(D);
-  if (mode == 7) {
+  if (mode == 7 || mode == 8) {
     if (workspace != nullptr && workspace_bytes >= cullavo_attn_bwd_workspace(B, H, Lq, Lk, D, dtype)) {
       u16* ds = (u16*)workspace;
-#define BDS(DD, CC) bwd_ds_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, ds, s)
+      const bool pipe = mode == 8;
+#define BDS(DD, CC) bwd_ds_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, ds, s, pipe)
       if (D == 128) return causal ? BDS(128, true) : BDS(128, false);
       return causal ? BDS(64, true) : BDS(64, false);
 #undef BDS

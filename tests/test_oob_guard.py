@@ -133,7 +133,7 @@ def test_attention_rows_past_end_next_to_nan(B, H, L, D, causal):
     prev_s = Lb.cullavo_attn_set_bwd_stage(0)
     try:
         base = None
-        for tiles in ((7, 4) if D == 128 else (0, 4)):
+        for tiles in ((7, 4, 8) if D == 128 else (0, 4, 8)):
             Lb.cullavo_attn_set_bwd_tiles(tiles)
             for st in (0, 1, 2, 3):
                 Lb.cullavo_attn_set_bwd_stage(st)

@@ -663,7 +663,9 @@ def test_attention_fwd_staging_modes_bitwise(B, H, L, D, causal, ks):
 def test_attention_bwd_tile_modes_bitwise(D, causal):
     """Every backward tile shape (cullavo_attn_set_bwd_tiles) sums the same products in the same
     order, so dQ/dK/dV agree bit for bit; ragged L and a left-padded batch row included. Mode 6
-    (64 keys per wave) keeps mode 0's per-key product order and is bitwise equal to it too."""
+    (64 keys per wave) keeps mode 0's per-key product order and is bitwise equal to it too. Mode 8
+    (software-pipelined dK/dV, one wave per SIMD) sums a key's queries in sweep order: within
+    bf16 rounding of mode 0, deterministic, and its dS^T (hence dQ) bitwise mode 7's."""
     from cullavo_amd import _lib
     B, H, L = 2, 3, 200
     q, k, v, do = (rnd((B * L, H * D), s).to(DEV) for s in (91, 92, 93, 94))
@@ -684,7 +686,7 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
     # mode 4 (8-wave kernels: the pair halves of each tile are summed once at the end) adds the
     # same products in another order: bf16-rounding-level differences only, and deterministic
     res8 = {}
-    for mode8 in (4, 5, 7):
+    for mode8 in (4, 5, 7, 8):
         _lib.lib().cullavo_attn_set_bwd_tiles(mode8)
         try:
             o4 = [t.clone() for t in ops().attn_bwd(q, k, v, o, do, lse, **kw)]
@@ -699,6 +701,9 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
     # mode 7 runs mode 4's dK/dV kernel (plus the dS^T stores): dK, dV bitwise equal to it
     for name, a, b in zip("kv", res8[4][1:], res8[7][1:]):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode 7 vs 4"
+    # mode 8 (the pipelined dK/dV kernel) writes the same dS^T values as mode 7, so the dQ that
+    # the shared dQ-from-dS kernel makes of them is bitwise mode 7's
+    assert torch.equal(res8[7][0].view(torch.int16), res8[8][0].view(torch.int16)), "dq mode 8 vs 7"
     # the LDS-DMA staging (cullavo_attn_set_bwd_stage) stages the same bytes (rows past the end as
     # zeros): modes 4 and 7 bitwise equal to the register staging, for the dK/dV kernel's Q / dO
     # (bit 0) and the dQ-from-dS kernel's K / dS^T (bit 1)

@@ -39,7 +39,7 @@ for stage in STAGES:
     tf = timeit(lambda: ops.attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5, causal=causal))
     res = []
     outs = {}
-    for mode in (4, 7, 1, 2):  # 4 = 8-wave dK/dV + 4-wave dQ, 7 = 8-wave dK/dV storing dS + dQ from it, 1 / 2 = 4-wave
+    for mode in (4, 7, 8, 1, 2):  # 4 = 8-wave dK/dV + 4-wave dQ, 7 = 8-wave dK/dV storing dS + dQ from it, 8 = 7 with the pipelined dK/dV, 1 / 2 = 4-wave
         _lib.lib().cullavo_attn_set_bwd_tiles(mode)
         tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=D ** -0.5,
                                          causal=causal, dq=dqkv[:, :H * D], dk=dqkv[:, H * D:2 * H * D],
@@ -47,7 +47,8 @@ for stage in STAGES:
         outs[mode] = dqkv.float().clone()
         res.append(f"m{mode} {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.1f} TF")
     diff = ((outs[4] - outs[1]).norm() / outs[1].norm()).item()
-    res.append(f"rel(m4, m1) {diff:.1e} rel(m7, m1) {((outs[7] - outs[1]).norm() / outs[1].norm()).item():.1e}")
+    res.append(f"rel(m4, m1) {diff:.1e} rel(m7, m1) {((outs[7] - outs[1]).norm() / outs[1].norm()).item():.1e} "
+               f"rel(m8, m1) {((outs[8] - outs[1]).norm() / outs[1].norm()).item():.1e}")
     key = name
     cur = (o.float().clone(), outs[7])
     if key in ref_out:

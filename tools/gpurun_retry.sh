@@ -1,7 +1,7 @@
 #!/bin/bash
 # gpurun, retried only while the pool has no free slot or box (nothing ran, nothing charged)
 out=$1; shift
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 24); do
   timeout 2400 /usr/local/graft/bin/gpurun "$@" > $out 2>&1
   if grep -q "nothing was charged\|no free box right now\|backing off" $out && ! grep -q "status=ok" $out; then
     sleep 150; continue
