@@ -2325,6 +2325,133 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
   }
 }
 
+// dQ from the stored dS, streaming form (mode 8): the kernel above reads its 0.3 GB of dS^T (7B
+// layer) with one tile of lookahead and a vmcnt(0) per tile, so every tile waits out an HBM
+// round trip (2.5 TB/s). Here a 3-slot ring (K tile + dS^T tile per slot, 96 KiB, one 8-wave
+// workgroup per CU) keeps two tiles in flight by LDS-DMA with a counted vmcnt, and the transposed
+// fragment reads are inline asm (the builtin would make hipcc wait for every in-flight DMA). Wave
+// w: queries 32 (w & 3) of the 128-query block, the D-half w >> 2 of dQ. Same products in the same
+// order per output as attn_bwd_dq_ds_k (bitwise equal).
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq_ds3_k(const u16* __restrict__ K, int64_t ldk,
+                                                            const u16* __restrict__ dST, int64_t ldst, int64_t st_bh,
+                                                            int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
+                                                            int Lq, int Lk, float scale,
+                                                            const int32_t* __restrict__ kv_start) {
+  constexpr int KT = 64, QB = 128;
+  constexpr int TK = KT * D * 2, TS = KT * QB * 2, SL = TK + TS;
+  constexpr int NS = KT / 16, ND = D / 32, NDW = ND / 2;  // k-steps per tile, dt per wave
+  constexpr int NPW = StageDMA1<KT, D, 8>::kPer + StageDMA1<KT, QB, 8>::kPer;  // DMA instrs per tile per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (Lq + QB - 1) / QB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qw = wave & 3, dh = wave >> 2;
+  const int q = qb * QB + qw * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * QB;
+
+  f32x16 dq[NDW];
+#pragma unroll
+  for (int i = 0; i < NDW; ++i) dq[i] = f32x16(0.f);
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * QB + QB);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  StageDMA1<KT, D, 8> dk_;
+  StageDMA1<KT, QB, 8> ds_;
+  dk_.prep(ldk, wave, lane);
+  ds_.prep(ldst, wave, lane);
+  auto dma = [&](int t, int sl) {
+    dk_.issue(Kb, ldk, t * KT, Lk, smem + sl * SL, wave);
+    ds_.issue(Sb, ldst, t * KT, LkP, smem + sl * SL + TK, wave);
+  };
+  // per-lane transposed-fragment offsets (k-step 0; k-step s at + 32 W s): K^T columns of this
+  // wave's dt blocks, dS^T columns of its 32 queries
+  const unsigned sbase = lds_addr(smem);
+  unsigned ko[NDW][2], so[2];
+  {
+    const int i = lane & 15, qq = i >> 2, p = i & 3;
+    const int r0 = 4 * hf + qq;
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) {
+      const int ch = (((dh * NDW + j) * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+      ko[j][0] = sbase + kv_off<D>(r0, ch) + 8 * (p & 1);
+      ko[j][1] = sbase + kv_off<D>(r0 + 8, ch) + 8 * (p & 1);
+    }
+    const int ch = ((qw * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+    so[0] = sbase + TK + kv_off<QB>(r0, ch) + 8 * (p & 1);
+    so[1] = sbase + TK + kv_off<QB>(r0 + 8, ch) + 8 * (p & 1);
+  }
+  // k-step S of the tile in slot base sb: its dS^T fragment and this wave's K^T fragments
+  auto rd = [&](auto s_c, unsigned sb, s16x4 (&f)[2 + 2 * NDW]) {
+    constexpr int S = decltype(s_c)::value;
+    rdtr<S * 32 * QB>(f[0], f[1], so[0] + sb, so[1] + sb);
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) rdtr<S * 32 * D>(f[2 + 2 * j], f[3 + 2 * j], ko[j][0] + sb, ko[j][1] + sb);
+  };
+  auto tie = [&](auto cnt_c, s16x4 (&f)[2 + 2 * NDW]) {
+    constexpr int CNT = decltype(cnt_c)::value;
+#pragma unroll
+    for (int j = 0; j < 2 + 2 * NDW; ++j) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[j]) : "n"(CNT) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mm = [&](s16x4 (&f)[2 + 2 * NDW]) {
+    const frag8 bs = cat_tr(f[0], f[1]);
+#pragma unroll
+    for (int j = 0; j < NDW; ++j)
+      dq[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat_tr(f[2 + 2 * j], f[3 + 2 * j]), bs, dq[j], 0, 0, 0);
+  };
+  constexpr int NR = 2 + 2 * NDW;  // tr reads per k-step
+
+  if (t0 < ntiles) {
+    dma(t0, 0);
+    if (t0 + 1 < ntiles) dma(t0 + 1, 1);
+    int sl = 0;
+    for (int t = t0; t < ntiles; ++t) {
+      // tile t landed (tile t+1 may stay in flight), every wave is done with slot (t-1) % 3
+      if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + 2 < ntiles) dma(t + 2, sl == 0 ? 2 : sl - 1);
+      const unsigned sb = (unsigned)(sl * SL);
+      s16x4 fa[NR], fb[NR];
+      rd(std::integral_constant<int, 0>{}, sb, fa);
+      rd(std::integral_constant<int, 1>{}, sb, fb);
+      tie(std::integral_constant<int, NR>{}, fa);
+      mm(fa);
+      rd(std::integral_constant<int, 2>{}, sb, fa);
+      tie(std::integral_constant<int, NR>{}, fb);
+      mm(fb);
+      rd(std::integral_constant<int, 3>{}, sb, fb);
+      tie(std::integral_constant<int, NR>{}, fa);
+      mm(fa);
+      tie(std::integral_constant<int, 0>{}, fb);
+      mm(fb);
+      sl = sl == 2 ? 0 : sl + 1;
+    }
+  }
+  if (q < Lq) {
+    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
+#pragma unroll
+    for (int j = 0; j < NDW; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = f2bf(dq[j][rr * 4 + e] * scale);
+        *reinterpret_cast<u16x4*>(dQb + (dh * NDW + j) * 32 + 8 * rr + 4 * hf) = w;
+      }
+  }
+}
+
 int64_t ds_rows(int Lk) { return cdiv(Lk, 128) * 128; }
 int64_t ds_cols(int Lq) { return cdiv(Lq, 128) * 128; }
 
@@ -2440,6 +2567,7 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
   attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
   const int smem_p = 3 * (2 * 32 * D * 2 + 512);
+  const int smem_q = 3 * (64 * D * 2 + 64 * 128 * 2);
   const int smem_b = 2 * (64 * D * 2 + 64 * 128 * 2);
   static bool once = false;
   if (!once) {
@@ -2448,6 +2576,7 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL, true>, smem_b);
     set_smem(attn_bwd_dkdv_pipe_k<D, CAUSAL>, smem_p);
+    set_smem(attn_bwd_dq_ds3_k<D, CAUSAL>, smem_q);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
@@ -2460,7 +2589,10 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
   else
     attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
-  if (g_bwd_stage & 2)
+  if (pipe)
+    attn_bwd_dq_ds3_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_q, s>>>(
+        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+  else if (g_bwd_stage & 2)
     attn_bwd_dq_ds_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
         k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   else
