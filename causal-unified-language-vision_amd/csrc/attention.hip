@@ -784,18 +784,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     k_group_mfma<NS, 4>(kb, qf, st[1]);
   };
 
-  // one tile: softmax of sp (tile t, scores in registers) beside S of tile t+1 (K slot KS, into
-  // sn; NEXT = false on the last tile: no S), then P V of tile t (V slot VS)
-  auto tile = [&](auto ks_c, auto vs_c, auto next_c, int t, f32x16 (&sp)[2], f32x16 (&sn)[2]) {
-    constexpr unsigned KO = decltype(ks_c)::value * TILE;
-    constexpr unsigned VO = decltype(vs_c)::value * TILE;
-    constexpr bool NEXT = decltype(next_c)::value;
-    if constexpr (NEXT) {
-      // V slot VS^1 was last read by tile t-1's P V, K slot KS^1 by tile t's S (both before the
-      // previous barrier)
-      dma_v(t + 1, decltype(vs_c)::value ^ 1);
-      if (t + 2 < ntiles) dma_k(t + 2, decltype(ks_c)::value ^ 1);
-    }
+  // Tile t's mask, row max and rescale decision, run on its scores before tile t's iteration (at
+  // the end of iteration t-1, or after the prologue's S): no control flow (the mask and rescale
+  // branches) may sit between an inline-asm LDS read and its counted wait, since the compiler
+  // may then copy the read's destination registers before the data has landed
+  float muse = 0.f;
+  auto prep = [&](int t, f32x16 (&sp)[2]) {
     const int kbase = t * KT;
     const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
     if (need_mask) {
@@ -816,50 +810,61 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
             sp[kt][r] = (unsigned)(koff + kt * 32 + acc_row(r, 0)) >= kspan ? -INFINITY : sp[kt][r];
       }
     }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[kt][r]);
+    tmax = swap_max(tmax) * c;
+    const bool grow = __any(tmax > m + rescale_thr);  // wave-uniform
+    const float mnew = grow ? fmaxf(m, tmax) : m;
+    muse = (mnew == -INFINITY) ? 0.f : mnew;
+    if (grow) {
+      const float alpha = fast_exp2(m - muse);
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) o[i] *= alpha;
+    }
+    m = mnew;
+  };
+
+  // one tile: P of sp (tile t, masked scores in registers, decision taken by prep) beside S of
+  // tile t+1 (K slot KS, into sn; NEXT = false on the last tile: no S), then P V of tile t (V slot
+  // VS), then prep of tile t+1
+  auto tile = [&](auto ks_c, auto vs_c, auto next_c, int t, f32x16 (&sp)[2], f32x16 (&sn)[2]) {
+    constexpr unsigned KO = decltype(ks_c)::value * TILE;
+    constexpr unsigned VO = decltype(vs_c)::value * TILE;
+    constexpr bool NEXT = decltype(next_c)::value;
+    if constexpr (NEXT) {
+      // V slot VS^1 was last read by tile t-1's P V, K slot KS^1 by tile t's S (both before the
+      // previous barrier)
+      dma_v(t + 1, decltype(vs_c)::value ^ 1);
+      if (t + 2 < ntiles) dma_k(t + 2, decltype(ks_c)::value ^ 1);
+    }
     // S of tile t+1 in NS groups of 2 MFMAs (K fragments 2 groups in flight), each group's issue
-    // gaps carrying one (D = 128) or two (D = 64) of the softmax chunks 0-7 of tile t
+    // gaps carrying one (D = 128) or two (D = 64) of the P chunks 0-7 of tile t
     s16x8 ka[2], kb[2];
     s16x4 lo0[ND], hi0[ND], lo1[ND], hi1[ND];
-    float tmax = -INFINITY, muse = 0.f, alpha = 1.f, rsE = 0.f, rsO = 0.f;
-    bool grow = false;
+    float rsE = 0.f, rsO = 0.f;
     frag8 pf[4];
+    const float nm = -muse;
     constexpr unsigned K1 = 32 * 2 * D;  // second 32-key half of the K tile
     constexpr int HG = NS / 2;           // groups per 32-key half
-    // softmax chunk C of tile t and its VALU count (the interleave pattern's filler per MFMA pair)
+    // P chunk C: registers 4 (C % 4) .. + 3 of score tile C / 4, the packed fragment when a
+    // 16-key slice is complete
     auto chunk = [&](auto c_c) {
       constexpr int C = decltype(c_c)::value;
-      if constexpr (C == 0) {
-        pin(sp[0]);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[0][r]);
-        pin(tmax);
-      } else if constexpr (C == 1) {
-        pin(sp[1]);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sp[1][r]);
-        tmax = swap_max(tmax) * c;
-        grow = __any(tmax > m + rescale_thr);
-        const float mnew = grow ? fmaxf(m, tmax) : m;
-        muse = (mnew == -INFINITY) ? 0.f : mnew;
-        alpha = grow ? fast_exp2(m - muse) : 1.f;
-        l *= alpha;
-        m = mnew;
-        pin(muse);
-        pin(l);
-      } else {
-        constexpr int KT_ = (C - 2) / 4, R0 = ((C - 2) % 4) * 4;
-        sm_exp4<KT_, R0>(sp, c, -muse, rsE, rsO);
-        if constexpr (R0 == 4 || R0 == 12) {
-          pf[2 * KT_ + R0 / 8] = pack_frag(sp[KT_], R0 / 8);
-          pin(pf[2 * KT_ + R0 / 8]);
-        }
+      constexpr int KT_ = C / 4, R0 = (C % 4) * 4;
+      sm_exp4<KT_, R0>(sp, c, nm, rsE, rsO);
+      if constexpr (R0 == 4 || R0 == 12) {
+        pf[2 * KT_ + R0 / 8] = pack_frag(sp[KT_], R0 / 8);
+        pin(pf[2 * KT_ + R0 / 8]);
       }
     };
-    constexpr int kFill[8] = {4, 6, 6, 8, 6, 8, 6, 8};
+    constexpr int kFill[8] = {6, 8, 6, 8, 6, 8, 6, 8};
     // group G: its MFMAs, its chunk(s), then the reads two groups ahead (or the first P V reads)
     auto group = [&](auto g_c) {
       constexpr int G = decltype(g_c)::value;
-      constexpr unsigned OFF = KO + (G / HG) * K1;
       constexpr int S0 = 2 * (G % HG);
       if constexpr (NEXT) {
         if constexpr (G % 2 == 0) {
@@ -885,7 +890,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
       } else {
         tr_group_issue<ND, VO + 16 * 2 * D>(lo1, hi1, toff);
       }
-      (void)OFF;
     };
     if constexpr (NEXT) {
       sn[0] = f32x16(0.f);
@@ -903,35 +907,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
       group(std::integral_constant<int, 6>{});
       group(std::integral_constant<int, 7>{});
     }
-    __builtin_amdgcn_sched_barrier(0);
-    if (grow) {
-#pragma unroll
-      for (int i = 0; i < ND; ++i) o[i] *= alpha;
-    }
-    // P V, slice 0 | P of registers 8-15 of score tile 1
+    // P V, slice 0 | the row sum
     tr_group_tie<ND, 2 * ND>(lo0, hi0);
     tr_group_mfma<ND>(lo0, hi0, pf[0], o);
-    sm_exp4<1, 8>(sp, c, -muse, rsE, rsO);
-    sm_exp4<1, 12>(sp, c, -muse, rsE, rsO);
-    pf[3] = pack_frag(sp[1], 1);
-    pin(pf[3]);
-    interleave<ND, 7>();
-    tr_group_issue<ND, VO + 32 * 2 * D>(lo0, hi0, toff);
-    // slice 1 | the row sum
-    tr_group_tie<ND, 2 * ND>(lo1, hi1);
-    tr_group_mfma<ND>(lo1, hi1, pf[1], o);
     {
       float rs = rsE + rsO;
       rs = swap_sum(rs);
       l += rs;
     }
     interleave<ND, 1>();
+    tr_group_issue<ND, VO + 32 * 2 * D>(lo0, hi0, toff);
+    tr_group_tie<ND, 2 * ND>(lo1, hi1);
+    tr_group_mfma<ND>(lo1, hi1, pf[1], o);
     tr_group_issue<ND, VO + 48 * 2 * D>(lo1, hi1, toff);
     tr_group_tie<ND, 2 * ND>(lo0, hi0);
     tr_group_mfma<ND>(lo0, hi0, pf[2], o);
     tr_group_tie<ND, 0>(lo1, hi1);
     tr_group_mfma<ND>(lo1, hi1, pf[3], o);
     if constexpr (NEXT) {
+      prep(t + 1, sn);
       // K t+2 / V t+1 landed (vmcnt counts LDS-DMA), and every wave's reads of the slots they
       // refill next iteration are done
       __builtin_amdgcn_sched_barrier(0);
@@ -948,6 +942,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     __builtin_amdgcn_s_waitcnt(kVmcnt0);
     __syncthreads();
     s_plain(std::integral_constant<int, 0>{}, sa);
+    prep(t0, sa);
     __syncthreads();  // K slot 0 is refilled (tile t0 + 2) by the first iteration
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -2003,14 +1998,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_k(
       for (int r = 0; r < 16; ++r)
         sc[r] = (unsigned)(qoff + acc_row(r, 0)) >= qspan ? -INFINITY : sc[r];
     }
-    // lse / delta quads of tile t (issued first: the first group's counted wait covers them)
-    s16x8 aux[8];
-    {
-      unsigned aa[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) aa[j] = sbase + cb + laux + 32 * (j & 3) + 256 * (j >> 2);
-      rd128<8, 0>(aux, aa);
-    }
+    // lse / delta quads of tile t, two per elementwise chunk, issued one group ahead of their chunk
+    // beside the fragment reads (few registers in flight: under register pressure the compiler
+    // parks long-lived asm outputs in AGPRs, copying them before the data has landed)
+    s16x8 auxa[2], auxb[2];
+    auto aux_issue = [&](auto rr_c, s16x8 (&f)[2]) {
+      constexpr int RR = decltype(rr_c)::value;
+      const unsigned a0 = sbase + cb + laux + 32 * RR;
+      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[0]) : "v"(a0) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:256" : "=&v"(f[1]) : "v"(a0) : "memory");
+    };
     s16x8 ga[4], gb[4];
     auto issue = [&](auto g_c, s16x8 (&f)[4]) {
       constexpr int G = decltype(g_c)::value;
@@ -2032,12 +2029,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_k(
     // elementwise chunk rr: accumulator registers 4 rr .. 4 rr + 3 (query rows 8 rr + 4 hf + 0..3)
     auto chunk = [&](auto rr_c) {
       constexpr int RR = decltype(rr_c)::value;
-      // the quads are valid only after the group's counted wait: every use stays below these pins
-      // (no pins on the S / dP accumulators: an asm operand would move them out of AGPRs)
-      pin(aux[RR]);
-      pin(aux[4 + RR]);
-      const f32x4 l4 = __builtin_bit_cast(f32x4, aux[RR]);
-      const f32x4 d4 = __builtin_bit_cast(f32x4, aux[4 + RR]);
+      // the quads are valid only after the group's counted wait, which ties them (no pins on the
+      // S / dP accumulators: an asm operand would move them out of AGPRs)
+      s16x8 (&ax)[2] = RR % 2 == 0 ? auxa : auxb;
+      const f32x4 l4 = __builtin_bit_cast(f32x4, ax[0]);
+      const f32x4 d4 = __builtin_bit_cast(f32x4, ax[1]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = RR * 4 + j;
@@ -2057,43 +2053,80 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_k(
         pin(df[S]);
       }
     };
-    if constexpr (NEXT) {
+    // waits: group g's 4 fragments and chunk g's 2 quads; the next group's 6 reads stay in flight
+    auto tie6 = [&](auto cnt_c, s16x8 (&f)[4], s16x8 (&ax)[2]) {
+      constexpr int CNT = decltype(cnt_c)::value;
+      asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(ax[0]), "+v"(ax[1])
+                   : "n"(CNT) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    using C3 = std::integral_constant<int, 3>;
+    using W6 = std::integral_constant<int, 6>;
+    using W0 = std::integral_constant<int, 0>;
+    if constexpr (NEXT && NG == 4) {
       sn = f32x16(0.f);
       pn = f32x16(0.f);
-      issue(std::integral_constant<int, 0>{}, ga);
-      issue(std::integral_constant<int, 1>{}, gb);
-      // group 0
-      tie128<4, 4>(ga);
-      mm(std::integral_constant<int, 0>{}, ga);
-      chunk(std::integral_constant<int, 0>{});
+      aux_issue(C0{}, auxa);
+      issue(C0{}, ga);
+      aux_issue(C1{}, auxb);
+      issue(C1{}, gb);
+      tie6(W6{}, ga, auxa);
+      mm(C0{}, ga);
+      chunk(C0{});
       interleave<4, 5>();
-      if constexpr (NG > 2) issue(std::integral_constant<int, 2 % NG>{}, ga);
-      // group 1
-      tie128<(NG > 2 ? 4 : 0), 4>(gb);
-      mm(std::integral_constant<int, 1>{}, gb);
-      chunk(std::integral_constant<int, 1>{});
+      aux_issue(C2{}, auxa);
+      issue(C2{}, ga);
+      tie6(W6{}, gb, auxb);
+      mm(C1{}, gb);
+      chunk(C1{});
       interleave<4, 9>();
-      if constexpr (NG > 2) {
-        issue(std::integral_constant<int, 3 % NG>{}, gb);
-        // groups 2, 3
-        tie128<4, 4>(ga);
-        mm(std::integral_constant<int, 2 % NG>{}, ga);
-        chunk(std::integral_constant<int, 2>{});
-        interleave<4, 5>();
-        tie128<0, 4>(gb);
-        mm(std::integral_constant<int, 3 % NG>{}, gb);
-        chunk(std::integral_constant<int, 3>{});
-        interleave<4, 9>();
-      } else {
-        chunk(std::integral_constant<int, 2>{});
-        chunk(std::integral_constant<int, 3>{});
-      }
+      aux_issue(C3{}, auxb);
+      issue(C3{}, gb);
+      tie6(W6{}, ga, auxa);
+      mm(C2{}, ga);
+      chunk(C2{});
+      interleave<4, 5>();
+      tie6(W0{}, gb, auxb);
+      mm(C3{}, gb);
+      chunk(C3{});
+      interleave<4, 9>();
+    } else if constexpr (NEXT) {  // D = 64: two groups of 4 MFMAs, chunks 2 and 3 after them
+      sn = f32x16(0.f);
+      pn = f32x16(0.f);
+      aux_issue(C0{}, auxa);
+      issue(C0{}, ga);
+      aux_issue(C1{}, auxb);
+      issue(C1{}, gb);
+      tie6(W6{}, ga, auxa);
+      mm(C0{}, ga);
+      chunk(C0{});
+      interleave<4, 5>();
+      aux_issue(C2{}, auxa);
+      tie6(std::integral_constant<int, 2>{}, gb, auxb);
+      mm(C1{}, gb);
+      chunk(C1{});
+      interleave<4, 9>();
+      aux_issue(C3{}, auxb);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
+      chunk(C2{});
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
+      chunk(C3{});
     } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      chunk(std::integral_constant<int, 0>{});
-      chunk(std::integral_constant<int, 1>{});
-      chunk(std::integral_constant<int, 2>{});
-      chunk(std::integral_constant<int, 3>{});
+      aux_issue(C0{}, auxa);
+      aux_issue(C1{}, auxb);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
+      chunk(C0{});
+      aux_issue(C2{}, auxa);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
+      chunk(C1{});
+      aux_issue(C3{}, auxb);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
+      chunk(C2{});
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
+      chunk(C3{});
     }
     __builtin_amdgcn_sched_barrier(0);
     // dV += P^T dO, dK += dS^T Q over tile t (slot cb): per (half s, column block dt) the dO and Q

@@ -22,7 +22,10 @@ using namespace cvgemm;
 
 constexpr int kGemvWaves = 8;
 constexpr int kGemvBatch = 16;  // W fragment loads per batch
-constexpr int kGemvDefault = 1;
+// the default variant (cvgemm_launch_gemv's switch): contiguous K ranges, 8-load batches at two
+// workgroups per CU -- 10-15 % faster than 16-load batches at one workgroup per CU on the 7B
+// decode products (profiles/r04/decode/gemv_variants.txt)
+constexpr int kGemvDefault = 4;
 
 // Decode-row input transforms fused into the X fragment loads (cullavo_decode_linear): XF 0 none;
 // 1 RMSNorm (x: the residual stream h [M, K]; each workgroup recomputes the M row statistics with
@@ -57,7 +60,8 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, f
 // ORDER 0: each wave a contiguous K range; ORDER 1: k-steps dealt round-robin over the 8 waves
 // (at any moment a workgroup reads one contiguous 512-B run per weight row); RB: 16-row blocks per
 // workgroup (each wave computes all of them over its k-steps). Measured alike on the 7B decode
-// step (ORDER 0 / 1: 4.14 / 4.16 ms per token; RB 2: 4.66-4.79, profiles/r04/decode/).
+// step (ORDER 0 / 1: 4.14 / 4.16 ms per token; RB 2: 4.66-4.79, profiles/r04/decode/); what
+// mattered was occupancy (NBW below).
 // NBW: W fragment loads per batch and wave. 16 keeps 151 VGPRs (one workgroup per CU: every
 // workgroup's load ramp and reduction are exposed); 8 fits 2 workgroups per CU (86 VGPRs) and
 // 4 fits 4, so one workgroup's ramp / reduction runs under the others' streams.
@@ -189,8 +193,8 @@ extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int6
   a.xf_w = (const u16*)norm_w;
   a.xf_eps = eps;
   const unsigned grid = (unsigned)cdiv(N, 16);
-  if (x_transform == 0) gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 0><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  else if (x_transform == 1) gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  else gemv_k<CULLAVO_DT_BF16, kGemvDefault, 1, 2><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  if (x_transform == 0) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  else if (x_transform == 1) gemv_k<CULLAVO_DT_BF16, 0, 1, 1, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, 2, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
   return cullavo_check_launch("decode_linear");
 }
