@@ -248,7 +248,7 @@ def decode_main(args):
         launches = ops.trace_launches()
         ops.trace_gemm(None)
         gv = [(k, ms) for k, ms in launches if k[0] <= 16 and k[3] == 0 and k[4] == 0]
-        g_bytes = sum(2.0 * (M * K + N * K + M * N) for (M, N, K, _, _), _ in gv)
+        g_bytes = sum(2.0 * (k[0] * k[2] + k[1] * k[2] + k[0] * k[1]) for k, _ in gv)
         g_ms = sum(ms for _, ms in gv)
         # timed: a fresh prefill, then n_tok graph replays
         torch.cuda.synchronize()
@@ -374,9 +374,10 @@ def cpu_baseline(cfg, text_len: int, budget_s: float):
                        f"ViT layers; {time.perf_counter() - t_start:.1f}s of CPU work")}
 
 
-def gemm_kernel_name(M, N, K, al=0, bl=0):
+def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
     """rocprof name (template arguments as rocprofv3 prints them) + workgroup count of the
-    kernel cullavo_gemm picks for a bf16-output problem (cullavo_gemm_plan)"""
+    kernel cullavo_gemm picks for a bf16-output problem (cullavo_gemm_plan); lora: the
+    instantiation with the fused LoRA up-projection (gemm256_k<..., LORA = true>)"""
     import ctypes
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
@@ -386,8 +387,11 @@ def gemm_kernel_name(M, N, K, al=0, bl=0):
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",
              10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
-             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1>"}
-    return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
+             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1, 0, 1, 0, 8>"}
+    name = names.get(tile, f"tile{tile}<{al}, {bl}>")
+    if lora and tile in (2, 10):
+        name = name[:-1] + ", true>"
+    return name, int(g.value)
 
 
 GEMM_ROLE = {(0, 0): "forward Y = X W^T", (0, 1): "input gradient dX = dY W", (1, 1): "weight gradient dW = dY^T X",
@@ -399,9 +403,12 @@ def gemm_families(launches):
     bytes (A + B read once, C written; + C read when accumulating is not traced: beta = 0 in the
     step) -> achieved TFLOP/s per kernel, sorted by GPU time."""
     fam = {}
-    for (M, N, K, al, bl), ms in launches:
-        name, _ = gemm_kernel_name(M, N, K, al, bl)
-        f = fam.setdefault(name, {"kernel": name, "role": GEMM_ROLE[(al, bl)], "launches": 0, "ms": 0.0,
+    for key, ms in launches:
+        M, N, K, al, bl = key[:5]
+        lora = len(key) > 5
+        name, _ = gemm_kernel_name(M, N, K, al, bl, lora)
+        role = GEMM_ROLE[(al, bl)] + (" + fused LoRA up-projection" if lora else "")
+        f = fam.setdefault(name, {"kernel": name, "role": role, "launches": 0, "ms": 0.0,
                                   "flops": 0.0, "bytes": 0.0, "shapes": set()})
         f["launches"] += 1
         f["ms"] += ms
@@ -418,13 +425,14 @@ def gemm_families(launches):
 def gemm_shapes(launches, steps, top=12):
     """per-shape GEMM time of the timed steps (the largest first): where each family's time goes"""
     sh = {}
-    for (M, N, K, al, bl), ms in launches:
-        r = sh.setdefault((M, N, K, al, bl), [0, 0.0])
+    for key, ms in launches:
+        r = sh.setdefault(tuple(key), [0, 0.0])
         r[0] += 1
         r[1] += ms
     out = []
-    for (M, N, K, al, bl), (n, ms) in sorted(sh.items(), key=lambda kv: -kv[1][1])[:top]:
-        name, grid = gemm_kernel_name(M, N, K, al, bl)
+    for key, (n, ms) in sorted(sh.items(), key=lambda kv: -kv[1][1])[:top]:
+        M, N, K, al, bl = key[:5]
+        name, grid = gemm_kernel_name(M, N, K, al, bl, len(key) > 5)
         out.append({"shape": f"{M}x{N}x{K}", "layouts": [al, bl], "kernel": name, "grid": grid,
                     "launches_per_step": round(n / steps, 2), "ms_per_step": round(ms / steps, 3),
                     "tflops": round(2.0 * M * N * K * n / (ms * 1e-3) / 1e12, 1)})

@@ -119,7 +119,9 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
          _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _stream())
     if traced:
         e1.record(torch.cuda.current_stream())
-        _TRACE["events"].append((e0, e1, (M, N, K, a_layout, b_layout)))
+        # the key names the kernel's problem; a 6th element marks the LoRA-fused instantiation
+        key = (M, N, K, a_layout, b_layout) if lora is None else (M, N, K, a_layout, b_layout, "lora")
+        _TRACE["events"].append((e0, e1, key))
     return C
 
 
@@ -185,7 +187,9 @@ def gemm_ex(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb
     call("gemm_ex", ctypes.addressof(d), _stream())
     if traced:
         e1.record(torch.cuda.current_stream())
-        _TRACE["events"].append((e0, e1, (M, N, K, a_layout, b_layout)))
+        # the key names the kernel's problem; a 6th element marks the LoRA-fused instantiation
+        key = (M, N, K, a_layout, b_layout) if lora is None else (M, N, K, a_layout, b_layout, "lora")
+        _TRACE["events"].append((e0, e1, key))
     return C
 
 
