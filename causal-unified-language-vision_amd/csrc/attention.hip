@@ -632,16 +632,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const u16* __restrict__ Q, 
 // vmcnt(0) -- the in-flight LDS-DMA -- in front of the builtin transposed read) and each
 // softmax chunk is pinned beside its MFMA group by sched_group_barrier. Per element the
 // arithmetic is attn_fwd_k's, in the same order: outputs bitwise equal to STAGE 4.
+// both wave halves' values of a per-query quantity combined (lane l with lane l ^ 32) by one
+// v_permlane32_swap on two registers holding x: afterwards one holds the lower half's values in
+// both halves, the other the upper half's. Inline asm, so the two operands are two registers: the
+// builtin given the same value twice may get one register for both, and then swaps nothing
+// useful (both results read back as the lower half: a doubled row sum). The 2 wait states a VALU
+// write needs before the swap reads it are the s_nop (cdna_hip_programming.md, permlane hazard).
+DEV void swap_halves(unsigned& a, unsigned& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
 DEV float swap_max(float x) {
-  // both wave halves' values, max of lane l and lane l ^ 32 (one v_permlane32_swap, no LDS)
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x),
-                                                  false, false);
-  return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+  unsigned a = __builtin_bit_cast(unsigned, x), b = a;
+  swap_halves(a, b);
+  return fmaxf(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b));
 }
 DEV float swap_sum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x),
-                                                  false, false);
-  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+  unsigned a = __builtin_bit_cast(unsigned, x), b = a;
+  swap_halves(a, b);
+  return __builtin_bit_cast(float, a) + __builtin_bit_cast(float, b);
 }
 // NM MFMAs, each followed by NV VALU instructions (the scheduler's placement of the group's code)
 template <int NM, int NV>
