@@ -304,6 +304,32 @@ DEV void tr_group_mfma(const s16x4 (&lo)[ND], const s16x4 (&hi)[ND], const frag8
   }
 }
 
+// two V^T fragments (column blocks DT0, DT0 + 1 of a 16-key slice at LDS offset VB) by inline asm,
+// tied by a counted lgkmcnt wait: the pipelined forward's P V reads in pairs (fewer registers in
+// flight than a whole slice: register pressure made the compiler spill in-flight fragments)
+template <int ND, unsigned VB, int DT0>
+DEV void tr2_issue(s16x4 (&lo)[2], s16x4 (&hi)[2], const unsigned (&toff)[ND][2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+                 : "=&v"(lo[j]), "=&v"(hi[j])
+                 : "v"(toff[DT0 + j][0]), "v"(toff[DT0 + j][1]), "n"(VB)
+                 : "memory");
+}
+template <int CNT>
+DEV void tr2_tie(s16x4 (&lo)[2], s16x4 (&hi)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int ND, int DT0>
+DEV void tr2_mfma(const s16x4 (&lo)[2], const s16x4 (&hi)[2], const frag8& pf, f32x16 (&o)[ND]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const s16x8 v = __builtin_shufflevector(lo[j], hi[j], 0, 1, 2, 3, 4, 5, 6, 7);
+    o[DT0 + j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, v), pf, o[DT0 + j], 0, 0, 0);
+  }
+}
+
 // ============================================================================================
 // forward
 // ============================================================================================
@@ -852,7 +878,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     // S of tile t+1 in NS groups of 2 MFMAs (K fragments 2 groups in flight), each group's issue
     // gaps carrying one (D = 128) or two (D = 64) of the P chunks 0-7 of tile t
     s16x8 ka[2], kb[2];
-    s16x4 lo0[ND], hi0[ND], lo1[ND], hi1[ND];
+    s16x4 la[2], ha[2], lb[2], hb[2];  // P V fragment pairs, two in flight
+    constexpr int PG = ND / 2;           // pairs per 16-key slice
+    constexpr int NPV = 4 * PG;          // P V groups
     float rsE = 0.f, rsO = 0.f;
     frag8 pf[4];
     const float nm = -muse;
@@ -876,10 +904,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
       constexpr int S0 = 2 * (G % HG);
       if constexpr (NEXT) {
         if constexpr (G % 2 == 0) {
-          k2_tie<G == NS - 1 ? 2 * ND : 2>(ka);
+          k2_tie<G == NS - 1 ? 4 : 2>(ka);
           k2_mfma<NS, S0>(ka, qf, sn[G / HG]);
         } else {
-          k2_tie<G == NS - 1 ? 2 * ND : 2>(kb);
+          k2_tie<G == NS - 1 ? 4 : 2>(kb);
           k2_mfma<NS, S0>(kb, qf, sn[G / HG]);
         }
       }
@@ -894,9 +922,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
           else k2_issue<NS, 2 * ((G + 2) % HG), OFF2>(kb, roff);
         }
       } else if constexpr (G == NS - 2) {
-        tr_group_issue<ND, VO + 0 * 2 * D>(lo0, hi0, toff);
+        tr2_issue<ND, VO, 0>(la, ha, toff);  // P V group 0
       } else {
-        tr_group_issue<ND, VO + 16 * 2 * D>(lo1, hi1, toff);
+        tr2_issue<ND, VO + (1 / PG) * 16 * 2 * D, 2 * (1 % PG)>(lb, hb, toff);  // P V group 1
       }
     };
     if constexpr (NEXT) {
@@ -915,23 +943,40 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
       group(std::integral_constant<int, 6>{});
       group(std::integral_constant<int, 7>{});
     }
-    // P V, slice 0 | the row sum
-    tr_group_tie<ND, 2 * ND>(lo0, hi0);
-    tr_group_mfma<ND>(lo0, hi0, pf[0], o);
-    {
-      float rs = rsE + rsO;
-      rs = swap_sum(rs);
-      l += rs;
+    // P V in NPV pair groups (slice v / PG, column blocks 2 (v % PG) + 0, 1), one group in flight
+    // under the current one's MFMAs; the row sum beside the first
+    auto pv = [&](auto v_c) {
+      constexpr int V = decltype(v_c)::value;
+      constexpr int CNT = V + 1 < NPV ? 4 : 0;
+      if constexpr (V % 2 == 0) {
+        tr2_tie<CNT>(la, ha);
+        tr2_mfma<ND, 2 * (V % PG)>(la, ha, pf[V / PG], o);
+      } else {
+        tr2_tie<CNT>(lb, hb);
+        tr2_mfma<ND, 2 * (V % PG)>(lb, hb, pf[V / PG], o);
+      }
+      if constexpr (V == 0) {
+        float rs = rsE + rsO;
+        rs = swap_sum(rs);
+        l += rs;
+        interleave<2, 2>();
+      }
+      if constexpr (V + 2 < NPV) {
+        constexpr unsigned VB = VO + ((V + 2) / PG) * 16 * 2 * D;
+        if constexpr (V % 2 == 0) tr2_issue<ND, VB, 2 * ((V + 2) % PG)>(la, ha, toff);
+        else tr2_issue<ND, VB, 2 * ((V + 2) % PG)>(lb, hb, toff);
+      }
+    };
+    pv(std::integral_constant<int, 0>{});
+    pv(std::integral_constant<int, 1>{});
+    pv(std::integral_constant<int, 2>{});
+    pv(std::integral_constant<int, 3>{});
+    if constexpr (NPV == 8) {
+      pv(std::integral_constant<int, 4>{});
+      pv(std::integral_constant<int, 5>{});
+      pv(std::integral_constant<int, 6>{});
+      pv(std::integral_constant<int, 7>{});
     }
-    interleave<ND, 1>();
-    tr_group_issue<ND, VO + 32 * 2 * D>(lo0, hi0, toff);
-    tr_group_tie<ND, 2 * ND>(lo1, hi1);
-    tr_group_mfma<ND>(lo1, hi1, pf[1], o);
-    tr_group_issue<ND, VO + 48 * 2 * D>(lo1, hi1, toff);
-    tr_group_tie<ND, 2 * ND>(lo0, hi0);
-    tr_group_mfma<ND>(lo0, hi0, pf[2], o);
-    tr_group_tie<ND, 0>(lo1, hi1);
-    tr_group_mfma<ND>(lo1, hi1, pf[3], o);
     if constexpr (NEXT) {
       prep(t + 1, sn);
       // K t+2 / V t+1 landed (vmcnt counts LDS-DMA), and every wave's reads of the slots they
