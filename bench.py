@@ -387,7 +387,7 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",
              10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
-             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1, 0, 1, 0, 8>"}
+             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: f"gemv_k<1, 0, 1, 0, {4 if K >= 8192 else 8}>"}
     name = names.get(tile, f"tile{tile}<{al}, {bl}>")
     if lora and tile in (2, 10):
         name = name[:-1] + ", true>"

@@ -798,24 +798,40 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     }
   }
 
-  // S = K Q^T of the K tile in slot SLOT, plain (prologue): 4 groups of 4 fragments
+  // S = K Q^T of the K tile in slot SLOT, plain (prologue): NS groups of 2 fragments (32-key half
+  // G / (NS / 2), k-steps 2 (G % (NS / 2)) + 0, 1), two groups in flight
   auto s_plain = [&](auto slot_c, f32x16 (&st)[2]) {
     constexpr unsigned KO = decltype(slot_c)::value * TILE;
-    s16x8 ka[4], kb[4];
+    constexpr int HG = NS / 2;
+    constexpr unsigned K1 = 32 * 2 * D;
+    s16x8 ka[2], kb[2];
     st[0] = f32x16(0.f);
     st[1] = f32x16(0.f);
-    k_group_issue<NS, 0, KO>(ka, roff);
-    k_group_issue<NS, 4, KO>(kb, roff);
-    k_group_tie<4>(ka);
-    k_group_mfma<NS, 0>(ka, qf, st[0]);
-    k_group_issue<NS, 0, KO + 32 * 2 * D>(ka, roff);
-    k_group_tie<4>(kb);
-    k_group_mfma<NS, 4>(kb, qf, st[0]);
-    k_group_issue<NS, 4, KO + 32 * 2 * D>(kb, roff);
-    k_group_tie<4>(ka);
-    k_group_mfma<NS, 0>(ka, qf, st[1]);
-    k_group_tie<0>(kb);
-    k_group_mfma<NS, 4>(kb, qf, st[1]);
+    auto grp = [&](auto g_c) {
+      constexpr int G = decltype(g_c)::value;
+      constexpr int CNT = G + 1 < NS ? 2 : 0;
+      if constexpr (G % 2 == 0) {
+        k2_tie<CNT>(ka);
+        k2_mfma<NS, 2 * (G % HG)>(ka, qf, st[G / HG]);
+        if constexpr (G + 2 < NS) k2_issue<NS, 2 * ((G + 2) % HG), KO + ((G + 2) / HG) * K1>(ka, roff);
+      } else {
+        k2_tie<CNT>(kb);
+        k2_mfma<NS, 2 * (G % HG)>(kb, qf, st[G / HG]);
+        if constexpr (G + 2 < NS) k2_issue<NS, 2 * ((G + 2) % HG), KO + ((G + 2) / HG) * K1>(kb, roff);
+      }
+    };
+    k2_issue<NS, 0, KO>(ka, roff);
+    k2_issue<NS, 2 * (1 % HG), KO + (1 / HG) * K1>(kb, roff);
+    grp(std::integral_constant<int, 0>{});
+    grp(std::integral_constant<int, 1>{});
+    grp(std::integral_constant<int, 2>{});
+    grp(std::integral_constant<int, 3>{});
+    if constexpr (NS == 8) {
+      grp(std::integral_constant<int, 4>{});
+      grp(std::integral_constant<int, 5>{});
+      grp(std::integral_constant<int, 6>{});
+      grp(std::integral_constant<int, 7>{});
+    }
   };
 
   // Tile t's mask, row max and rescale decision, run on its scores before tile t's iteration (at

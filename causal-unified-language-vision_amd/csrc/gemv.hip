@@ -152,7 +152,10 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   // lab switch (CULLAVO_GEMV: 0 contiguous K ranges, 1 round-robin k-steps, 2 / 3 = 0 / 1 with
   // 32 rows per workgroup, 4 / 5 = 0 / 1 with 8-load batches at 2 workgroups per CU, 6 / 7 = 0 / 1
   // with 4-load batches at 4 workgroups per CU), read once per process
-  static const int v = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : kGemvDefault;
+  static const int venv = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : -1;
+  // default: 8-load batches; 4-load batches (four workgroups per CU) for the long-K products
+  // (down: 20.9 vs 21.9 us at batch 1, 22.5 vs 24.6 at batch 8, gemv_variants.txt)
+  const int v = venv >= 0 ? venv : (p.K >= 8192 ? 6 : kGemvDefault);
   const int rb = (v == 2 || v == 3) ? 2 : 1;
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
   GemvArgs a{};
