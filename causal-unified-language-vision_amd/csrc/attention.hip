@@ -839,6 +839,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
   // branches) may sit between an inline-asm LDS read and its counted wait, since the compiler
   // may then copy the read's destination registers before the data has landed
   float muse = 0.f;
+  float alpha_p = 1.f;  // the pending rescale of l, folded into the next row-sum add
   auto prep = [&](int t, f32x16 (&sp)[2]) {
     const int kbase = t * KT;
     const bool need_mask = (CAUSAL && kbase + KT - 1 > qb * 128) || kbase + KT > Lk || kbase < kstart;
@@ -869,9 +870,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     const bool grow = __any(tmax > m + rescale_thr);  // wave-uniform
     const float mnew = grow ? fmaxf(m, tmax) : m;
     muse = (mnew == -INFINITY) ? 0.f : mnew;
+    alpha_p = 1.f;
     if (grow) {
       const float alpha = fast_exp2(m - muse);
-      l *= alpha;
+      alpha_p = alpha;
 #pragma unroll
       for (int i = 0; i < ND; ++i) o[i] *= alpha;
     }
@@ -974,7 +976,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
       if constexpr (V == 0) {
         float rs = rsE + rsO;
         rs = swap_sum(rs);
-        l += rs;
+        // l = l alpha + rs in one rounding, as attn_fwd_k's contracted l *= alpha; ...; l += rs
+        // (alpha = 1 when the max held: an exact add)
+        l = __builtin_fmaf(l, alpha_p, rs);
         interleave<2, 2>();
       }
       if constexpr (V + 2 < NPV) {
