@@ -99,8 +99,11 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // range-checked buffer loads, 2 = per-tile descriptor (StageT), 3 = 2 + s_setprio, 4 = LDS-DMA
 // (StageDMA, the default since round 3: 138.3 -> 132.0 us on the 7B layer, 153.3 -> 141.9 us on
 // the ViT bs-64 layer, alternating on one MI355X, profiles/r03/s3a/attn_bench.txt), 5 = 4 with
-// inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B)
-int g_fwd_stage = 4;
+// inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B), 7 = the
+// software-pipelined kernel attn_fwd_pipe_k (round 4); -1 (default) = 7 at D = 128 (7B layer
+// 140-152 -> 120-121 us), 4 at D = 64 (the ViT layer, 149-166 us against 161-183 with 7: its
+// half-width MFMAs leave too few issue gaps for the softmax), profiles/r04/attn/
+int g_fwd_stage = -1;
 // backward staging (cullavo_attn_set_bwd_stage): bit 0 = dK/dV Q / dO by LDS-DMA, bit 1 = the
 // dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT)
 int g_bwd_stage = 0;
@@ -2584,19 +2587,20 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
     once = true;
   }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  if (g_fwd_stage == 7)
+  const int stage = g_fwd_stage >= 0 ? g_fwd_stage : (D == 128 ? 7 : 4);
+  if (stage == 7)
     attn_fwd_pipe_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 6)
+  else if (stage == 6)
     attn_fwd_k<D, CAUSAL, 6><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 5)
+  else if (stage == 5)
     attn_fwd_k<D, CAUSAL, 5><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 4)
+  else if (stage == 4)
     attn_fwd_k<D, CAUSAL, 4><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 3)
+  else if (stage == 3)
     attn_fwd_k<D, CAUSAL, 2, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 2)
+  else if (stage == 2)
     attn_fwd_k<D, CAUSAL, 2><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
-  else if (g_fwd_stage == 1)
+  else if (stage == 1)
     attn_fwd_k<D, CAUSAL, 1><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   else
     attn_fwd_k<D, CAUSAL, 0><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
@@ -2740,7 +2744,7 @@ int g_bwd_tiles = -1;
 
 extern "C" int cullavo_attn_set_stage(int buffer_loads) {
   const int prev = g_fwd_stage;
-  if (buffer_loads >= 0 && buffer_loads <= 7) g_fwd_stage = buffer_loads;
+  if (buffer_loads >= -1 && buffer_loads <= 7) g_fwd_stage = buffer_loads;
   return prev;
 }
 

@@ -290,7 +290,10 @@ size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype
    waves w and w+4 split each query tile and add their partial sums once, in a fixed order)
    with the 4-wave 32-key dQ kernel; 5 = both kernels 8-wave; 0-3 = the 4-wave kernels;
    6 = 64 keys per wave dK/dV (4 waves, one per SIMD; bitwise equal to 0-3); 7 = mode 4's dK/dV
-   kernel storing dS^T + dQ from it (needs the cullavo_attn_bwd_ws workspace);
+   kernel storing dS^T + dQ from it (needs the cullavo_attn_bwd_ws workspace); 8 = mode 7's
+   products with the software-pipelined dK/dV kernel (one wave per SIMD, K / V in registers,
+   a 3-slot Q / dO ring; the same dS^T values, dK / dV summed in sweep order: bitwise equal to
+   mode 1) and the streaming dQ-from-dS kernel (3-slot ring, two tiles in flight);
    -1 (the default) = 7 for D=128 (4 through cullavo_attn_bwd, which has no workspace), 2 for
    D=64 (measured per head dim).
    In 0-3 with bit 0 = 64 query rows per dK/dV barrier, bit 1 = 64
@@ -301,10 +304,12 @@ int cullavo_attn_set_bwd_tiles(int mode);
    through a per-tile scalar descriptor (one loop-invariant lane offset, rows past the sequence
    end zero-filled by the range check), 1 = buffer loads with per-chunk offsets and range selects,
    0 = pointer loads behind a per-chunk bounds branch, 3 = mode 2 with the two MFMA blocks of a
-   K/V tile at raised wave priority (s_setprio; A/B experiment), 4 (default) = K/V tiles by
+   K/V tile at raised wave priority (s_setprio; A/B experiment), 4 = K/V tiles by
    LDS-DMA (buffer_load ... lds) straight into the swizzled LDS image (no staging registers, no
    ds_write), 5 = mode 4 with the K and V^T fragment reads as inline-asm groups of 4 under
-   counted lgkmcnt waits (the next group in flight while the current one's MFMAs issue).
+   counted lgkmcnt waits (the next group in flight while the current one's MFMAs issue), 7 = the
+   software-pipelined kernel (tile t's softmax in the issue gaps of tile t+1's S MFMAs, K / V in
+   rings of their own), -1 (the default) = 7 at D = 128, 4 at D = 64.
    Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
