@@ -119,8 +119,7 @@ def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C
          _ptr(bias), act, _ptr(preact), _ptr(residual), ldr, float(beta), _stream())
     if traced:
         e1.record(torch.cuda.current_stream())
-        # the key names the kernel's problem; a 6th element marks the LoRA-fused instantiation
-        key = (M, N, K, a_layout, b_layout) if lora is None else (M, N, K, a_layout, b_layout, "lora")
+        key = (M, N, K, a_layout, b_layout)
         _TRACE["events"].append((e0, e1, key))
     return C
 
