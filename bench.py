@@ -408,7 +408,7 @@ def gemm_families(launches):
         lora = len(key) > 5
         name, _ = gemm_kernel_name(M, N, K, al, bl, lora)
         role = GEMM_ROLE[(al, bl)] + (" + fused LoRA up-projection" if lora else "")
-        f = fam.setdefault(name, {"kernel": name, "role": role, "launches": 0, "ms": 0.0,
+        f = fam.setdefault(name, {"kernel": name, "role": role, "layouts": (al, bl), "launches": 0, "ms": 0.0,
                                   "flops": 0.0, "bytes": 0.0, "shapes": set()})
         f["launches"] += 1
         f["ms"] += ms
@@ -461,7 +461,7 @@ def gemm_ceiling(fam, iters=10):
 
     from cullavo_amd import ops
     (M, N, K) = max(fam["shapes"], key=lambda s: s[0] * s[1] * s[2])
-    al, bl = next(k for k, v in GEMM_ROLE.items() if v == fam["role"])
+    al, bl = fam["layouts"]
     g = torch.Generator(device="cuda").manual_seed(0)
     A = torch.randn((K, M) if al else (M, K), device="cuda", generator=g).bfloat16()
     B = torch.randn((K, N) if bl else (N, K), device="cuda", generator=g).bfloat16()
