@@ -279,10 +279,13 @@ def decode_main(args):
                                f"(L0={L0}), batch {B}, greedy, one HIP-graph replay per token",
                    "model": "llava-1.5-7b", "global_batch": B, "seq_len": L0, "parallelism": "dp1"},
         "prefill_ms": round(prefill_ms, 2), "weight_bytes": wbytes,
-        "roofline": {"kernel": f"gemv_k<1>: decode Linears Y = X W^T at M = {B}, {n_launch // 4} launches per step "
+        "roofline": {"kernel": f"{gemm_kernel_name(B, 4096, 4096)[0]} / {gemm_kernel_name(B, 4096, 11008)[0]}: decode "
+                             f"Linears Y = X W^T at M = {B}, {n_launch // 4} launches per step "
                                f"(eager step, HIP events per launch)",
                      "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                     "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "frac": round(achieved / 8000.0, 4), "traffic": measured_traffic("gemv_k<", f"decode-b{B}")[0],
+                     "traffic_unit": "bytes/launch averaged over every GEMV dispatch of one profiled decode run "
+                                     "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE; profiles/roofline_traffic.json)",
                      "algorithmic_bytes": round(g_bytes / max(n_launch, 1)),
                      "avg_ms": round(g_ms / max(n_launch, 1), 5)},
         "step_roofline": {"what": "LM + head weight bytes per token step / replayed step time (every kernel of the "
