@@ -386,15 +386,14 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
     g = ctypes.c_int64(0)
     tile = _lib.lib().cullavo_gemm_plan(M, N, K, al, bl, ctypes.byref(g))
     ldr = 0 if (al == 1 and os.environ.get("CULLAVO_GEMM_LOADERS") == "1") else 1  # gemm.hip default_ldr
-    names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0>",
-             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}>",
-             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}> split-K + splitk_reduce_k<1>",
-             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
+    # the 256-row kernels' last template argument is the fused-LoRA flag (rocprofv3 prints it)
+    lf = "true" if lora else "false"
+    names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0, false>",
+             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}, false>",
+             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, false> split-K + splitk_reduce_k<1>",
+             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}, {lf}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
              13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: f"gemv_k<1, 0, 1, 0, {4 if K >= 8192 else 8}>"}
-    name = names.get(tile, f"tile{tile}<{al}, {bl}>")
-    if lora and tile in (2, 10):
-        name = name[:-1] + ", true>"
-    return name, int(g.value)
+    return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 
 GEMM_ROLE = {(0, 0): "forward Y = X W^T", (0, 1): "input gradient dX = dY W", (1, 1): "weight gradient dW = dY^T X",
