@@ -250,6 +250,52 @@ __global__ __launch_bounds__(256) void rope8_k(T* __restrict__ q, int64_t ldq, T
   }
 }
 
+// RoPE of the decode step's new rows fused with the KV-cache append (cullavo_rope_kv_append):
+// rope8_k's arithmetic on q (in place) and k, the rotated k written straight to its cache row
+// (b, start[b] + t % Lnew) instead of back into the projection output, and v copied beside it --
+// one launch and one pass over k instead of rope8_k + kv_append_k (decode.hip).
+__global__ __launch_bounds__(256) void rope_append8_k(u16* __restrict__ q, int64_t ldq, const u16* __restrict__ k,
+                                                      int64_t ldk, const u16* __restrict__ v, int64_t ldv,
+                                                      const int64_t* __restrict__ pos, int hq, int hk, int D,
+                                                      float theta, u16* __restrict__ kc, u16* __restrict__ vc,
+                                                      int64_t ld_tok, int64_t ld_b, const int32_t* __restrict__ start,
+                                                      int Lnew) {
+  __shared__ float cs[256], sn[256];
+  const int64_t t = blockIdx.x;
+  const int half = D / 2, ng = half / 8;
+  if (threadIdx.x < half) {
+    const int i = threadIdx.x;
+    const float inv_freq = 1.0f / powf(theta, (float)(2 * i) / (float)D);
+    const float ang = (float)pos[t] * inv_freq;
+    cs[i] = Elt<u16>::rnd(cosf(ang));
+    sn[i] = Elt<u16>::rnd(sinf(ang));
+  }
+  __syncthreads();
+  const int b = (int)(t / Lnew), tt = (int)(t % Lnew);
+  const int64_t crow = (int64_t)b * ld_b + (int64_t)(start[b] + tt) * ld_tok;
+  const int nq = hq * ng, nall = (hq + hk) * ng;
+  for (int it = threadIdx.x; it < nall; it += 256) {
+    const bool isq = it < nq;
+    const int w = isq ? it : it - nq, h = w / ng, g8 = (w % ng) * 8;
+    const int64_t col = (int64_t)h * D + g8;
+    const u16* s1 = isq ? q + t * ldq + col : k + t * ldk + col;
+    u16* d1 = isq ? q + t * ldq + col : kc + crow + col;
+    float x1[8], x2[8], o1[8], o2[8];
+    load8(s1, x1);
+    load8(s1 + half, x2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = cs[g8 + j], sv = sn[g8 + j];
+      o1[j] = Elt<u16>::rnd(Elt<u16>::rnd(x1[j] * c) + Elt<u16>::rnd(-x2[j] * sv));
+      o2[j] = Elt<u16>::rnd(Elt<u16>::rnd(x2[j] * c) + Elt<u16>::rnd(x1[j] * sv));
+    }
+    store8(d1, o1);
+    store8(d1 + half, o2);
+  }
+  for (int c8 = threadIdx.x * 8; c8 < hk * D; c8 += 256 * 8)
+    *reinterpret_cast<u16x8*>(vc + crow + c8) = *reinterpret_cast<const u16x8*>(v + t * ldv + c8);
+}
+
 // ---- optimiser ------------------------------------------------------------------------------
 // block b sums a fixed grid-stride subset in a fixed order (lane accumulation, then the wave
 // tree, then waves 0..3) into partials[b]; sumsq_final_k adds the partials to out[0] in a
@@ -433,6 +479,24 @@ extern "C" int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const in
   else if (dtype == CULLAVO_DT_F32) rope_k<float><<<(unsigned)tokens, 256, 0, s>>>((float*)q, ldq, (float*)k, ldk, position_ids, hq, hk, head_dim, theta, inverse);
   else CV_REQUIRE(false, CULLAVO_EUNSUPPORTED, "dtype");
   return cullavo_check_launch("rope");
+}
+
+extern "C" int cullavo_rope_kv_append(void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                                      const int64_t* position_ids, int64_t tokens, int hq, int hk, int head_dim,
+                                      float theta, void* k_cache, void* v_cache, int64_t ld_tok, int64_t ld_b,
+                                      const int32_t* start, int Lnew, int dtype, void* stream) {
+  CV_REQUIRE(dtype == CULLAVO_DT_BF16, CULLAVO_EUNSUPPORTED, "rope_kv_append: bf16");
+  CV_REQUIRE(head_dim % 16 == 0 && head_dim <= 512 && Lnew >= 1 && tokens % Lnew == 0, CULLAVO_EINVAL,
+             "rope_kv_append: head_dim a multiple of 16 up to 512, tokens = B * Lnew");
+  CV_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ld_tok % 8 == 0 && ld_b % 8 == 0 &&
+                 (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)k_cache | (uintptr_t)v_cache) & 15) == 0,
+             CULLAVO_EINVAL, "rope_kv_append: 16-byte aligned rows");
+  if (tokens == 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  rope_append8_k<<<(unsigned)tokens, 256, 0, s>>>((u16*)q, ldq, (const u16*)k, ldk, (const u16*)v, ldv, position_ids, hq,
+                                                  hk, head_dim, theta, (u16*)k_cache, (u16*)v_cache, ld_tok, ld_b,
+                                                  start, Lnew);
+  return cullavo_check_launch("rope_kv_append");
 }
 
 extern "C" int cullavo_sumsq(const void* x, int64_t n, float* out, float* partials, int dtype, void* stream) {

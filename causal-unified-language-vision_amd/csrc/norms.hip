@@ -11,7 +11,10 @@ constexpr int kRowsPerBlock = 4;   // 4 waves, one row each
 constexpr int kBwdBlocks = 256;    // backward grid (weight-grad partials: 1024 wave slots)
 
 // ------------------------------------------------------------------------------------------
-template <typename T, int NCH>
+// PREW (few rows: the KV-cache decode step's one row per sequence): the weight row is loaded
+// together with x, before the reduction, so a launch waits out one memory round trip instead of
+// two (7.4 us per decode-step norm at one row; the many-row training launches keep the registers)
+template <typename T, int NCH, bool PREW = false>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                      T* __restrict__ y, float* __restrict__ rstd,
                                                      int64_t rows, int cols, float eps) {
@@ -20,12 +23,20 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, co
   if (row >= rows) return;
   const T* xr = x + row * cols;
   float v[NCH][8];
+  float wp[PREW ? NCH : 1][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = c * 512 + lane * 8;
     if (col < cols) {
       load8(xr + col, v[c]);
+      if constexpr (PREW) load8(w + col, wp[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < cols) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
     }
@@ -39,7 +50,12 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, co
     const int col = c * 512 + lane * 8;
     if (col < cols) {
       float wv[8], o[8];
-      load8(w + col, wv);
+      if constexpr (PREW) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wv[j] = wp[c][j];
+      } else {
+        load8(w + col, wv);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = wv[j] * Elt<T>::rnd(v[c][j] * r);
       store8(yr + col, o);
@@ -537,7 +553,9 @@ extern "C" int cullavo_rmsnorm_fwd(const void* x, const void* w, void* y, float*
   const int nb = (int)cdiv(rows, kRowsPerBlock);
   hipStream_t s = CV_STREAM(stream);
   const int nch = nch_for(cols);
-  if (dtype == CULLAVO_DT_BF16) {
+  if (dtype == CULLAVO_DT_BF16 && rows <= 64 && nch <= 8) {
+    NCH_DISPATCH(nch, rmsnorm_fwd_k<u16, NC, true><<<nb, 256, 0, s>>>((const u16*)x, (const u16*)w, (u16*)y, rstd, rows, (int)cols, eps));
+  } else if (dtype == CULLAVO_DT_BF16) {
     NCH_DISPATCH(nch, rmsnorm_fwd_k<u16, NC><<<nb, 256, 0, s>>>((const u16*)x, (const u16*)w, (u16*)y, rstd, rows, (int)cols, eps));
   } else if (dtype == CULLAVO_DT_F32) {
     NCH_DISPATCH(nch, rmsnorm_fwd_k<float, NC><<<nb, 256, 0, s>>>((const float*)x, (const float*)w, (float*)y, rstd, rows, (int)cols, eps));

@@ -131,8 +131,13 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
         t, _ = lg["qkv"].forward(x1, False, 0)
         qkv = ops.linear(x1, layer.w_qkv(), addend=t)
     q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
-    ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
-    ops.kv_append(k, v, cache.k[li], cache.v[li], start, B=B, Lnew=Lnew)
+    if Lnew == 1 and qkv.dtype == torch.bfloat16:
+        # decode: rotated k goes straight to the cache (one launch for RoPE + append)
+        ops.rope_kv_append(q, k, v, sctx.position_ids, cache.k[li], cache.v[li], start, hq=H, head_dim=D,
+                           theta=cfg.rope_theta, B=B, Lnew=1)
+    else:
+        ops.rope(q, k, sctx.position_ids, hq=H, hk=H, head_dim=D, theta=cfg.rope_theta)
+        ops.kv_append(k, v, cache.k[li], cache.v[li], start, B=B, Lnew=Lnew)
     if Lnew > 1:
         o, _ = ops.attn_fwd(q, k, v, B=B, H=H, Lq=Lnew, Lk=Lnew, D=D, scale=D ** -0.5, causal=True,
                             kv_start=sctx.kv_start)

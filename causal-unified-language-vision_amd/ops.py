@@ -396,6 +396,17 @@ def attn_fwd(q, k, v, *, B: int, H: int, Lq: int, Lk: int, D: int, scale: float,
     return o, lse
 
 
+def rope_kv_append(q, k, v, position_ids, k_cache, v_cache, start, *, hq: int, head_dim: int, theta: float,
+                   B: int, Lnew: int):
+    """cullavo_rope_kv_append: rope(q, k) in place on q, the rotated k and v appended to the caches
+    (k itself is left unrotated); bitwise rope() + kv_append()."""
+    _dev(q, k, v, position_ids, k_cache, v_cache, start)
+    hd = k_cache.shape[-1]
+    call("rope_kv_append", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(position_ids), B * Lnew, hq,
+         hd // head_dim, head_dim, float(theta), _ptr(k_cache), _ptr(v_cache), k_cache.stride(1), k_cache.stride(0),
+         _ptr(start), Lnew, _dt(q), _stream())
+
+
 def kv_append(k, v, k_cache, v_cache, start, *, B: int, Lnew: int):
     """k, v: [B*Lnew, >=hd] row-strided views; caches [B, Lmax, hd]; start int32 [B]."""
     _dev(k, v, k_cache, v_cache, start)

@@ -256,6 +256,16 @@ size_t cullavo_colsum_workspace(int64_t rows, int64_t cols);
 int cullavo_rope(void* q, int64_t ldq, void* k, int64_t ldk, const int64_t* position_ids,
                  int64_t tokens, int hq, int hk, int head_dim, float theta, int inverse,
                  int dtype, void* stream);
+/* The decode step's RoPE fused with the KV-cache append (reference: the cached branch of
+ * tf:llama LlamaAttention.forward, rotary embedding then DynamicCache.update): cullavo_rope's
+ * forward rotation on q (in place) and k, the rotated k written to k_cache row start[b] + t % Lnew
+ * of sequence b = t / Lnew (token stride ld_tok, batch stride ld_b) instead of back into k, and v
+ * copied to v_cache there -- bitwise cullavo_rope followed by cullavo_kv_append. bf16, head_dim a
+ * multiple of 16, 16-byte aligned rows. */
+int cullavo_rope_kv_append(void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                           const int64_t* position_ids, int64_t tokens, int hq, int hk, int head_dim,
+                           float theta, void* k_cache, void* v_cache, int64_t ld_tok, int64_t ld_b,
+                           const int32_t* start, int Lnew, int dtype, void* stream);
 
 /* ---- attention (flash-style, MFMA bf16) --------------------------------------------------
  * Replaces tf:llama/modeling_llama.py:191-282 (causal, D=128, FA2 in the reference,

@@ -322,3 +322,31 @@ def test_decode_linear_fused_transforms_bitwise(M):
     assert (y.float() - z).abs().max().item() <= 8e-3 * z.abs().max().item()
     with pytest.raises(ValueError):
         ops.decode_linear(torch.zeros(17, d, dtype=BF, device="cuda"), Wq)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lnew", [1, 2])
+def test_rope_kv_append_bitwise(Lnew):
+    """cullavo_rope_kv_append (the decode step's RoPE + cache append in one launch) leaves q and
+    the caches bitwise as cullavo_rope followed by cullavo_kv_append: q / k / v as column blocks of
+    one fused projection output, per-sequence cache rows start[b], ragged positions."""
+    import torch
+    from cullavo_amd import ops
+    B, H, D, Lmax = 3, 4, 128, 40
+    d = H * D
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(B * Lnew, 3 * d, generator=g).bfloat16().cuda()
+    pos = torch.tensor([7, 19, 33, 2, 5, 30][:B * Lnew], dtype=torch.int64).cuda()
+    start = torch.tensor([3, 0, 17], dtype=torch.int32).cuda()
+    caches = [torch.randn(B, Lmax, d, generator=g).bfloat16().cuda() for _ in range(2)]
+    a = qkv.clone()
+    ka, va = caches[0].clone(), caches[1].clone()
+    ops.rope(a[:, :d], a[:, d:2 * d], pos, hq=H, hk=H, head_dim=D, theta=10000.0)
+    ops.kv_append(a[:, d:2 * d], a[:, 2 * d:], ka, va, start, B=B, Lnew=Lnew)
+    b2 = qkv.clone()
+    kb, vb = caches[0].clone(), caches[1].clone()
+    ops.rope_kv_append(b2[:, :d], b2[:, d:2 * d], b2[:, 2 * d:], pos, kb, vb, start, hq=H, head_dim=D, theta=10000.0,
+                       B=B, Lnew=Lnew)
+    torch.cuda.synchronize()
+    assert torch.equal(a[:, :d], b2[:, :d])
+    assert torch.equal(ka, kb) and torch.equal(va, vb)
