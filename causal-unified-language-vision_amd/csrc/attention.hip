@@ -1146,14 +1146,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k(
   // lse / delta of a query tile (threads 0..2QT-1, one value each): loaded together with the
   // tile's Q / dO prefetch and written to LDS with them (not loaded and waited for at the end)
   float aux = 0.f;
+  // the next tile's lse / delta: loaded raw and first used when staged after the tile's compute
+  // (arithmetic on the loaded value at load time made the compiler wait for it -- and for the
+  // in-flight tile prefetch -- at the top of every tile)
+  bool aux_in = false;
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
       const int qq = qt * QT + (int)threadIdx.x % QT;
-      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+      aux_in = qq < Lq;
+      aux = (threadIdx.x < QT ? lseb : delb)[min(qq, Lq - 1)];
     }
   };
   auto store_aux = [&](char* buf) {
-    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TILE))[threadIdx.x] = aux;
+    if (threadIdx.x < 2 * QT)
+      ((float*)(buf + 2 * TILE))[threadIdx.x] = aux_in ? aux : (threadIdx.x < QT ? INFINITY : 0.f);
   };
   if (block_live && qt0 < nqt) {
     sq.load(Qb, ldq, qt0 * QT, Lq);
@@ -1454,14 +1460,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     ddo_.prep(lddo, wave, lane);
   }
   float aux = 0.f;
+  // the next tile's lse / delta: loaded raw and first used when staged after the tile's compute
+  // (the lse * log2 e at load time made the compiler wait for the load -- and for the in-flight
+  // Q / dO prefetch -- at the top of every tile)
+  bool aux_in = false;
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
       const int qq = qt * QT + (int)threadIdx.x % QT;
-      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] * kLog2e : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+      aux_in = qq < Lq;
+      aux = (threadIdx.x < QT ? lseb : delb)[min(qq, Lq - 1)];
     }
   };
   auto store_aux = [&](char* buf) {
-    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TQ))[threadIdx.x] = aux;
+    if (threadIdx.x < 2 * QT)
+      ((float*)(buf + 2 * TQ))[threadIdx.x] =
+          threadIdx.x < QT ? (aux_in ? aux * kLog2e : INFINITY) : (aux_in ? aux : 0.f);
   };
   if (block_live) {
     StageN<KB, D, 512> skv;
@@ -1777,14 +1790,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w64_k(
 
   StageN<QT, D, 256> sq, sdo;
   float aux = 0.f;
+  // the next tile's lse / delta: loaded raw and first used when staged after the tile's compute
+  // (the lse * log2 e at load time made the compiler wait for the load -- and for the in-flight
+  // Q / dO prefetch -- at the top of every tile)
+  bool aux_in = false;
   auto load_aux = [&](int qt) {
     if (threadIdx.x < 2 * QT) {
       const int qq = qt * QT + (int)threadIdx.x % QT;
-      aux = (threadIdx.x < QT) ? (qq < Lq ? lseb[qq] * kLog2e : INFINITY) : (qq < Lq ? delb[qq] : 0.f);
+      aux_in = qq < Lq;
+      aux = (threadIdx.x < QT ? lseb : delb)[min(qq, Lq - 1)];
     }
   };
   auto store_aux = [&](char* buf) {
-    if (threadIdx.x < 2 * QT) ((float*)(buf + 2 * TQ))[threadIdx.x] = aux;
+    if (threadIdx.x < 2 * QT)
+      ((float*)(buf + 2 * TQ))[threadIdx.x] =
+          threadIdx.x < QT ? (aux_in ? aux * kLog2e : INFINITY) : (aux_in ? aux : 0.f);
   };
   if (block_live) {
 #pragma unroll
