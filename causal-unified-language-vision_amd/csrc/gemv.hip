@@ -65,16 +65,18 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, f
 // NBW: W fragment loads per batch and wave. 16 keeps 151 VGPRs (one workgroup per CU: every
 // workgroup's load ramp and reduction are exposed); 8 fits 2 workgroups per CU (86 VGPRs) and
 // 4 fits 4, so one workgroup's ramp / reduction runs under the others' streams.
-template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : NBW >= 8 ? 4 : 8))) void gemv_k(GemvArgs a) {
+// NW: waves per workgroup (K split NW ways); 16 for the N = 4096 products, whose 256 workgroups
+// are one per CU whatever the occupancy allows
+template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : NBW >= 8 ? 4 : 8))) void gemv_k(GemvArgs a) {
   const GemmArgs& p = a.g;
-  __shared__ f32x4 red[kGemvWaves][RB][64];
+  __shared__ f32x4 red[NW][RB][64];
   __shared__ float rs[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n0 = (int64_t)blockIdx.x * 16 * RB;
   const int64_t nk = cdiv(p.K, 32);
-  const int64_t per = cdiv(nk, kGemvWaves);
+  const int64_t per = cdiv(nk, NW);
   const int r = lane & 15, g = lane >> 4;
   const u16* wrow[RB];
 #pragma unroll
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ?
     frag8 w[NB][RB], x[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * kGemvWaves + wave;
+      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * NW + wave;
       const int64_t kend = ORDER == 0 ? min(nk, (int64_t)(wave + 1) * per) : nk;
       const int64_t k = ks * 32 + 8 * g;  // this lane's first k of the step
       const bool in = j0 + i < per && ks < kend && k < p.K;
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ?
       // RMSNorm row statistics, after the first batch of weight loads is in flight: rmsnorm_fwd_k's
       // arithmetic (one wave per row, the same summation order), handed over through LDS with a
       // barrier that waits on the LDS only (the weight loads stay in flight)
-      for (int row = wave; row < p.M; row += kGemvWaves) {
+      for (int row = wave; row < p.M; row += NW) {
         const u16* xr = p.A + row * p.lda;
         float ss = 0.f;
         for (int c = 0; c * 512 < p.K; ++c) {
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ?
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * kGemvWaves + wave;
+      const int64_t ks = ORDER == 0 ? wave * per + j0 + i : (j0 + i) * NW + wave;
       const int64_t kend = ORDER == 0 ? min(nk, (int64_t)(wave + 1) * per) : nk;
       const int64_t k = ks * 32 + 8 * g;
       const bool in = j0 + i < per && ks < kend && k < p.K;
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ?
   if (wave < RB) {
     f32x4 s = red[0][wave][lane];
 #pragma unroll
-    for (int w2 = 1; w2 < kGemvWaves; ++w2) s += red[w2][wave][lane];
+    for (int w2 = 1; w2 < NW; ++w2) s += red[w2][wave][lane];
     store4<CT>(p, s, r, n0 + 16 * wave + 4 * g);
   }
 }
@@ -156,6 +158,7 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   // default: 8-load batches; 4-load batches (four workgroups per CU) for the long-K products
   // (down: 20.9 vs 21.9 us at batch 1, 22.5 vs 24.6 at batch 8, gemv_variants.txt)
   const int v = venv >= 0 ? venv : (p.K >= 8192 ? 6 : kGemvDefault);
+  // lab variants 8 / 9: 16 waves per workgroup with 4- / 8-load batches
   const int rb = (v == 2 || v == 3) ? 2 : 1;
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
   GemvArgs a{};
@@ -163,9 +166,13 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
 #define GV(O, R, NBW)                                                                                 \
   if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);                    \
   else gemv_k<CULLAVO_DT_BF16, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+#define GV16(NBW)                                                                                     \
+  if (f32) gemv_k<CULLAVO_DT_F32, 0, 1, 0, NBW, 16><<<grid, 64 * 16, 0, s>>>(a);                        \
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, 0, NBW, 16><<<grid, 64 * 16, 0, s>>>(a);
   if (v == 0) { GV(0, 1, 16) } else if (v == 1) { GV(1, 1, 16) } else if (v == 2) { GV(0, 2, 16) }
   else if (v == 3) { GV(1, 2, 16) } else if (v == 4) { GV(0, 1, 8) } else if (v == 5) { GV(1, 1, 8) }
-  else if (v == 6) { GV(0, 1, 4) } else { GV(1, 1, 4) }
+  else if (v == 6) { GV(0, 1, 4) } else if (v == 7) { GV(1, 1, 4) } else if (v == 8) { GV16(4) } else { GV16(8) }
+#undef GV16
 #undef GV
   return cullavo_check_launch("gemv");
 }
