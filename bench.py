@@ -392,7 +392,7 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}, false>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, false> split-K + splitk_reduce_k<1>",
              10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}, {lf}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
-             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: f"gemv_k<1, 0, 1, 0, {4 if K >= 8192 else 8}>"}
+             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 

@@ -157,8 +157,10 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   static const int venv = getenv("CULLAVO_GEMV") ? atoi(getenv("CULLAVO_GEMV")) : -1;
   // default: 8-load batches; 4-load batches (four workgroups per CU) for the long-K products
   // (down: 20.9 vs 21.9 us at batch 1, 22.5 vs 24.6 at batch 8, gemv_variants.txt)
-  const int v = venv >= 0 ? venv : (p.K >= 8192 ? 6 : kGemvDefault);
-  // lab variants 8 / 9: 16 waves per workgroup with 4- / 8-load batches
+  // 16 waves per workgroup with 4-load batches (variant 8) for the widest products (gate|up,
+  // lm_head: 34.5 vs 35.5 us and 45.2 vs 46.8 at batch 1, profiles/r04/decode/gemv_variants16.txt);
+  // lab variant 9: 16 waves with 8-load batches (slower)
+  const int v = venv >= 0 ? venv : (p.K >= 8192 ? 6 : p.N > 16384 ? 8 : kGemvDefault);
   const int rb = (v == 2 || v == 3) ? 2 : 1;
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
   GemvArgs a{};
