@@ -1040,19 +1040,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(const u16* __restrict_
     }
   }
 
-  if (q < Lq) {
+  // O rows, widened stores (cdna_hip_programming.md T21): lanes l and l ^ 32 hold the two
+  // 4-column halves of each 8-column group of the same row; one v_permlane32_swap per dword of a
+  // pair of groups (k, k+1) leaves the lower half-wave with columns 8k..8k+7 and the upper with
+  // 8k+8..8k+15, one 16-B store each instead of two 8-B stores. The swaps run on every lane (a
+  // lane and its partner hold the same query row, so the row guard is uniform across the pair).
+  {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     u16* Ob = O + ((int64_t)b * Lq + q) * ldo + (int64_t)h * D;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        u16x4 wv;
+      for (int rr = 0; rr < 4; rr += 2) {
+        u16x4 wa, wb;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wv[j] = f2bf(o[dt][rr * 4 + j] * inv);
-        *reinterpret_cast<u16x4*>(Ob + dt * 32 + 8 * rr + 4 * hf) = wv;
+        for (int j = 0; j < 4; ++j) {
+          wa[j] = f2bf(o[dt][rr * 4 + j] * inv);
+          wb[j] = f2bf(o[dt][(rr + 1) * 4 + j] * inv);
+        }
+        u32x2 a = __builtin_bit_cast(u32x2, wa), bb = __builtin_bit_cast(u32x2, wb);
+        unsigned ax = a[0], ay = a[1], bx = bb[0], by = bb[1];
+        swap_halves(ax, bx);
+        swap_halves(ay, by);
+        if (q < Lq) {
+          const u32x4 w4 = {ax, ay, bx, by};
+          *reinterpret_cast<u32x4*>(Ob + dt * 32 + 8 * rr + 8 * hf) = w4;
+        }
       }
-    if (hf == 0) LSE[((int64_t)b * H + h) * Lq + q] = l > 0.f ? (m + log2f(l)) * kLn2 : INFINITY;
+    if (q < Lq && hf == 0) LSE[((int64_t)b * H + h) * Lq + q] = l > 0.f ? (m + log2f(l)) * kLn2 : INFINITY;
   }
 }
 
