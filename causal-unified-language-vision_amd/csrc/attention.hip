@@ -100,9 +100,9 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // (StageDMA, the default since round 3: 138.3 -> 132.0 us on the 7B layer, 153.3 -> 141.9 us on
 // the ViT bs-64 layer, alternating on one MI355X, profiles/r03/s3a/attn_bench.txt), 5 = 4 with
 // inline-asm fragment groups (131.7 / 141.1 us: within noise of 4, kept as an A/B), 7 = the
-// software-pipelined kernel attn_fwd_pipe_k (round 4); -1 (default) = 7 at D = 128 (7B layer
-// 140-152 -> 120-121 us), 4 at D = 64 (the ViT layer, 149-166 us against 161-183 with 7: its
-// half-width MFMAs leave too few issue gaps for the softmax), profiles/r04/attn/
+// software-pipelined kernel attn_fwd_pipe_k (round 4); -1 (default) = 7 (with its widened O
+// stores: 7B layer 151 -> 124-128 us, ViT bs-64 layer 148-154 -> 139-144 us alternating on one
+// box, profiles/r04/attn/attn_fwd_ab.txt)
 int g_fwd_stage = -1;
 // backward staging (cullavo_attn_set_bwd_stage): bit 0 = dK/dV Q / dO by LDS-DMA, bit 1 = the
 // dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT)
@@ -2622,7 +2622,7 @@ int fwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
     once = true;
   }
   const unsigned grid = (unsigned)(cdiv(Lq, 128) * H * B);
-  const int stage = g_fwd_stage >= 0 ? g_fwd_stage : (D == 128 ? 7 : 4);
+  const int stage = g_fwd_stage >= 0 ? g_fwd_stage : 7;
   if (stage == 7)
     attn_fwd_pipe_k<D, CAUSAL><<<grid, 256, smem, s>>>(q, ldq, k, ldk, v, ldv, o, ldo, lse, H, Lq, Lk, scale, ks);
   else if (stage == 6)

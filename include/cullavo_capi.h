@@ -319,7 +319,7 @@ int cullavo_attn_set_bwd_tiles(int mode);
    ds_write), 5 = mode 4 with the K and V^T fragment reads as inline-asm groups of 4 under
    counted lgkmcnt waits (the next group in flight while the current one's MFMAs issue), 7 = the
    software-pipelined kernel (tile t's softmax in the issue gaps of tile t+1's S MFMAs, K / V in
-   rings of their own), -1 (the default) = 7 at D = 128, 4 at D = 64.
+   rings of their own), -1 (the default) = 7.
    Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
