@@ -51,98 +51,123 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
   if (kbeg >= kend) {  // chunk past this row's length: empty partial
     if (t < D) part_o[pidx * D + t] = 0.f;
     if (t == 0) { part_ml[2 * pidx] = -INFINITY; part_ml[2 * pidx + 1] = 0.f; }
-    return;
+  } else {
+    if (t < D) qs[t] = bf2f(Q[(int64_t)b * ldq + (int64_t)h * D + t]) * scale_log2;
+    const u16* Kb = Kc + (int64_t)b * ld_b + (int64_t)h * D;
+    const u16* Vb = Vc + (int64_t)b * ld_b + (int64_t)h * D;
+    // scores: 8 lanes per key (16 dims each, one 256 B row per key), 32 keys per pass; the K rows
+    // and the V rows of P.V (which do not depend on the scores) are all in flight before the first
+    // is consumed
+    const int sub = t & 7, slot = t >> 3;
+    constexpr int kPass = kChunk / 32;
+    u16x8 kr[kPass][2];
+#pragma unroll
+    for (int pass = 0; pass < kPass; ++pass) {
+      const int key = min(kbeg + pass * 32 + slot, kend - 1);
+      const u16* kp = Kb + (int64_t)key * ld_tok + sub * 16;
+      kr[pass][0] = *reinterpret_cast<const u16x8*>(kp);
+      kr[pass][1] = *reinterpret_cast<const u16x8*>(kp + 8);
+    }
+    // P.V: thread (dim group dg of 8 dims, key group kg) sums keys kg, kg+16, ...
+    const int dg = t & 15, kg = t >> 4;
+    const int nk = kend - kbeg;
+    u16x8 vr[kChunk / 16];
+#pragma unroll
+    for (int i = 0; i < kChunk / 16; ++i) {
+      const int k = min(kg + 16 * i, nk - 1);
+      vr[i] = *reinterpret_cast<const u16x8*>(Vb + (int64_t)(kbeg + k) * ld_tok + dg * 8);
+    }
+    __syncthreads();
+    float qv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) qv[j] = qs[sub * 16 + j];
+#pragma unroll
+    for (int pass = 0; pass < kPass; ++pass) {
+      const int key = kbeg + pass * 32 + slot;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += qv[j] * bf2f(kr[pass][0][j]) + qv[8 + j] * bf2f(kr[pass][1][j]);
+      acc += __shfl_xor(acc, 1);
+      acc += __shfl_xor(acc, 2);
+      acc += __shfl_xor(acc, 4);
+      if (sub == 0) ps[pass * 32 + slot] = (key < kend && key >= k_lo) ? acc : -INFINITY;
+    }
+    __syncthreads();
+    // chunk max and sum (kChunk = 128 scores, threads >= 128 carry -inf / 0)
+    const int lane = t & 63, wv = t >> 6;
+    const float s = t < kChunk ? ps[t] : -INFINITY;
+    float m = wave_max(s);
+    if (lane == 0) red[wv] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const float p = (s == -INFINITY) ? 0.f : exp2f(s - m);
+    __syncthreads();
+    if (t < kChunk) ps[t] = p;
+    float l = wave_sum(p);
+    if (lane == 0) red[4 + wv] = l;
+    __syncthreads();
+    l = red[4] + red[5] + red[6] + red[7];
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < kChunk / 16; ++i) {
+      const int k = kg + 16 * i;
+      const float pk = k < nk ? ps[k] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += pk * bf2f(vr[i][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) oacc[kg][dg * 8 + j] = o[j];
+    __syncthreads();
+    if (t < D) {
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) sum += oacc[g][t];
+      part_o[pidx * D + t] = sum;
+    }
+    if (t == 0) { part_ml[2 * pidx] = m; part_ml[2 * pidx + 1] = l; }
   }
-  if (t < D) qs[t] = bf2f(Q[(int64_t)b * ldq + (int64_t)h * D + t]) * scale_log2;
-  __syncthreads();
-  const u16* Kb = Kc + (int64_t)b * ld_b + (int64_t)h * D;
-  const u16* Vb = Vc + (int64_t)b * ld_b + (int64_t)h * D;
-  // scores: 8 lanes per key (16 dims each, one 256 B row per key), 32 keys per pass; all the
-  // passes' loads are issued before any is consumed
-  const int sub = t & 7, slot = t >> 3;
-  constexpr int kPass = kChunk / 32;
-  u16x8 kr[kPass][2];
-#pragma unroll
-  for (int pass = 0; pass < kPass; ++pass) {
-    const int key = min(kbeg + pass * 32 + slot, kend - 1);
-    const u16* kp = Kb + (int64_t)key * ld_tok + sub * 16;
-    kr[pass][0] = *reinterpret_cast<const u16x8*>(kp);
-    kr[pass][1] = *reinterpret_cast<const u16x8*>(kp + 8);
-  }
-  float qv[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) qv[j] = qs[sub * 16 + j];
-#pragma unroll
-  for (int pass = 0; pass < kPass; ++pass) {
-    const int key = kbeg + pass * 32 + slot;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += qv[j] * bf2f(kr[pass][0][j]) + qv[8 + j] * bf2f(kr[pass][1][j]);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    acc += __shfl_xor(acc, 4);
-    if (sub == 0) ps[pass * 32 + slot] = (key < kend && key >= k_lo) ? acc : -INFINITY;
-  }
-  __syncthreads();
-  // chunk max and sum (kChunk = 128 scores, threads >= 128 carry -inf / 0)
-  const int lane = t & 63, wv = t >> 6;
-  const float s = t < kChunk ? ps[t] : -INFINITY;
-  float m = wave_max(s);
-  if (lane == 0) red[wv] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float p = (s == -INFINITY) ? 0.f : exp2f(s - m);
-  __syncthreads();
-  if (t < kChunk) ps[t] = p;
-  float l = wave_sum(p);
-  if (lane == 0) red[4 + wv] = l;
-  __syncthreads();
-  l = red[4] + red[5] + red[6] + red[7];
-  // P.V: thread (dim group dg of 8 dims, key group kg) sums keys kg, kg+16, ...
-  const int dg = t & 15, kg = t >> 4;
-  const int nk = kend - kbeg;
-  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  u16x8 vr[kChunk / 16];
-#pragma unroll
-  for (int i = 0; i < kChunk / 16; ++i) {
-    const int k = min(kg + 16 * i, nk - 1);
-    vr[i] = *reinterpret_cast<const u16x8*>(Vb + (int64_t)(kbeg + k) * ld_tok + dg * 8);
-  }
-#pragma unroll
-  for (int i = 0; i < kChunk / 16; ++i) {
-    const int k = kg + 16 * i;
-    const float pk = k < nk ? ps[k] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] += pk * bf2f(vr[i][j]);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) oacc[kg][dg * 8 + j] = o[j];
-  __syncthreads();
-  if (t < D) {
-    float sum = 0.f;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) sum += oacc[g][t];
-    part_o[pidx * D + t] = sum;
-  }
-  if (t == 0) { part_ml[2 * pidx] = m; part_ml[2 * pidx + 1] = l; }
 }
 
+// Combine: max over the chunks, then the rescaled sums in chunk order (deterministic). Up to
+// kCombineRegs chunks (max_len <= 2048) every partial is loaded before the first is used.
+constexpr int kCombineRegs = 16;
 template <int D>
 __global__ __launch_bounds__(D) void attn_decode_combine_k(const float* __restrict__ part_o,
                                                           const float* __restrict__ part_ml, u16* __restrict__ O,
                                                           int64_t ldo, int H, int nchunk) {
   const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int64_t base = ((int64_t)b * H + h) * nchunk;
-  float M = -INFINITY;
-  for (int c = 0; c < nchunk; ++c) M = fmaxf(M, part_ml[2 * (base + c)]);
-  float L = 0.f, acc = 0.f;
-  if (M != -INFINITY) {
-    for (int c = 0; c < nchunk; ++c) {
-      const float mc = part_ml[2 * (base + c)];
-      if (mc == -INFINITY) continue;
-      const float w = exp2f(mc - M);
-      L += w * part_ml[2 * (base + c) + 1];
-      acc += w * part_o[(base + c) * D + d];
+  float M = -INFINITY, L = 0.f, acc = 0.f;
+  if (nchunk <= kCombineRegs) {
+    float mc[kCombineRegs], lc[kCombineRegs], oc[kCombineRegs];
+#pragma unroll
+    for (int c = 0; c < kCombineRegs; ++c) {
+      const bool in = c < nchunk;
+      mc[c] = in ? part_ml[2 * (base + c)] : -INFINITY;
+      lc[c] = in ? part_ml[2 * (base + c) + 1] : 0.f;
+      oc[c] = in ? part_o[(base + c) * D + d] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < kCombineRegs; ++c) M = fmaxf(M, mc[c]);
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int c = 0; c < kCombineRegs; ++c) {
+        if (mc[c] == -INFINITY) continue;
+        const float w = exp2f(mc[c] - M);
+        L += w * lc[c];
+        acc += w * oc[c];
+      }
+    }
+  } else {
+    for (int c = 0; c < nchunk; ++c) M = fmaxf(M, part_ml[2 * (base + c)]);
+    if (M != -INFINITY) {
+      for (int c = 0; c < nchunk; ++c) {
+        const float mc = part_ml[2 * (base + c)];
+        if (mc == -INFINITY) continue;
+        const float w = exp2f(mc - M);
+        L += w * part_ml[2 * (base + c) + 1];
+        acc += w * part_o[(base + c) * D + d];
+      }
     }
   }
   O[(int64_t)b * ldo + (int64_t)h * D + d] = f2bf(L > 0.f ? acc / L : 0.f);  // no visible key -> 0
