@@ -108,12 +108,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
       for (int row = wave; row < p.M; row += NW) {
         const u16* xr = p.A + row * p.lda;
         float ss = 0.f;
-        for (int c = 0; c * 512 < p.K; ++c) {
-          const int col = c * 512 + lane * 8;
-          if (col < p.K) {
-            const u16x8 xv = *reinterpret_cast<const u16x8*>(xr + col);
+        // 8 row loads in flight per round (one round at K = 4096): a load-use loop here costs a
+        // memory round trip per 512 columns, which every wave of the workgroup waits for
+        for (int c0 = 0; c0 * 512 < p.K; c0 += 8) {
+          u16x8 xv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ss += bf2f(xv[j]) * bf2f(xv[j]);
+          for (int c = 0; c < 8; ++c) {
+            const int col = (c0 + c) * 512 + lane * 8;
+            xv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(xr + col) : u16x8{};
+          }
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const int col = (c0 + c) * 512 + lane * 8;
+            if (col < p.K) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) ss += bf2f(xv[c][j]) * bf2f(xv[c][j]);
+            }
           }
         }
         ss = wave_sum(ss);
@@ -205,8 +215,14 @@ extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int6
   a.xf_w = (const u16*)norm_w;
   a.xf_eps = eps;
   const unsigned grid = (unsigned)cdiv(N, 16);
-  if (x_transform == 0) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  else if (x_transform == 1) gemv_k<CULLAVO_DT_BF16, 0, 1, 1, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  else gemv_k<CULLAVO_DT_BF16, 0, 1, 2, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  // the shapes' variants as cvgemm_launch_gemv picks them: 16 waves x 4-load batches for the widest
+  // products, 4-load batches for K >= 8192, else 8-load batches
+  const int v = K >= 8192 ? 6 : N > 16384 ? 8 : kGemvDefault;
+#define DL(XF)                                                                                        \
+  if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16><<<grid, 64 * 16, 0, s>>>(a);                      \
+  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4><<<grid, 64 * kGemvWaves, 0, s>>>(a);             \
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  if (x_transform == 0) { DL(0) } else if (x_transform == 1) { DL(1) } else { DL(2) }
+#undef DL
   return cullavo_check_launch("decode_linear");
 }

@@ -24,7 +24,14 @@ from . import ops
 from .functions import StepContext
 from .lora import NO_LORA
 
-FUSE_DECODE_NORMS = False
+import os
+
+# decode-step fusions into the weight-streaming products (cullavo_decode_linear): "norm" folds the
+# two RMSNorms into the q|k|v and gate|up products' X loads, "swiglu" the SwiGLU into down_proj's
+# (both bitwise the unfused values); CULLAVO_DECODE_FUSE="norm,swiglu" / "norm" / "" (none)
+_FUSE = {f.strip() for f in os.environ.get("CULLAVO_DECODE_FUSE", "").split(",") if f.strip()}
+FUSE_DECODE_NORMS = "norm" in _FUSE
+FUSE_DECODE_SWIGLU = "swiglu" in _FUSE
 
 
 class KVCache:
@@ -117,10 +124,11 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
     lg = layer.lora_groups
     B = sctx.B
-    # FUSE_DECODE_NORMS: the norms and the SwiGLU inside the weight-streaming products
-    # (cullavo_decode_linear transforms 1 / 2, bitwise the unfused values) -- measured 1.8-2.2x slower
-    # per product than the separate kernels (every workgroup repeats the row transform; 7B step
-    # 7.06 vs 4.05 ms at batch 1, profiles/r04/decode/), so off
+    # FUSE_DECODE_NORMS / _SWIGLU: the norms and the SwiGLU inside the weight-streaming products
+    # (cullavo_decode_linear transforms 1 / 2, bitwise the unfused values) -- measured ~2x slower per
+    # product than the separate kernels: a workgroup streams only two weight batches, and the row
+    # statistics (or the SwiGLU) put a dependent memory round trip in front of its first MFMA (7B step
+    # 7.01 / 7.81 vs 3.69 ms at batch 1, profiles/r04/decode/decode_fusions_ab.txt), so off
     fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] <= 16 and h.dtype == torch.bfloat16
              and all(g is NO_LORA for g in lg.values()))
     if fused:
@@ -150,7 +158,9 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     if fused:
         gu = ops.decode_linear(h2, layer.w_gu(), transform=1, norm_w=layer.post_attention_layernorm.weight,
                                eps=cfg.rms_norm_eps)
-        return ops.decode_linear(gu, layer.mlp.down_proj.weight, transform=2, residual=h2)
+        if FUSE_DECODE_SWIGLU:
+            return ops.decode_linear(gu, layer.mlp.down_proj.weight, transform=2, residual=h2)
+        return ops.linear(ops.swiglu_fwd(gu), layer.mlp.down_proj.weight, residual=h2)
     x2, _ = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
     t, _ = lg["gu"].forward(x2, False, 0)
     gu = ops.linear(x2, layer.w_gu(), addend=t)

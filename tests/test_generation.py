@@ -268,6 +268,27 @@ def test_decode_graph_matches_eager_steps():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_decode_fusions_bitwise(monkeypatch, swiglu):
+    """The decode layer with its RMSNorms (and SwiGLU) folded into the weight-streaming products
+    (CULLAVO_DECODE_FUSE) gives bitwise the logits of the separate kernels, step after step."""
+    from cullavo_amd import generation
+    cfg = O.config_small_gpu()
+    m = _model(6)
+    ids, mask, pix, _ = O.make_inputs(cfg, 2, 20, 3, 31)
+    ids, mask, pix = ids.cuda(), mask.cuda(), pix.cuda()
+    toks = torch.randint(2, cfg.image_token_index, (4, 2), generator=torch.Generator().manual_seed(5)).cuda()
+    runs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(generation, "FUSE_DECODE_NORMS", fuse)
+        monkeypatch.setattr(generation, "FUSE_DECODE_SWIGLU", fuse and swiglu)
+        cache = m(input_ids=ids, pixel_values=pix, attention_mask=mask, use_cache=True).past_key_values
+        runs.append([m(input_ids=t[:, None], past_key_values=cache, use_cache=True).logits.clone() for t in toks])
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), i
+
+
+@pytest.mark.gpu
 def test_generate_eos_stop_with_sparse_checks():
     """generate() tests 'all rows finished' every 16 tokens and trims the padding-only steps it ran
     past the stop: the result equals the per-step-checked loop (an eos that every row emits)."""
@@ -317,6 +338,11 @@ def test_decode_linear_fused_transforms_bitwise(M):
         a = ops.decode_linear(gu, Wd, transform=2, residual=r)
         b = ops.decode_linear(act, Wd, residual=r)
         assert torch.equal(a, b)
+    # the widest product (gate|up: 16-wave workgroups) and the plain linear's dispatch agree too
+    Wgu = (torch.randn(2 * F, d, generator=g) * d ** -0.5).to(BF).cuda()
+    a = ops.decode_linear(h, Wgu, transform=1, norm_w=nw, eps=1e-5)
+    assert torch.equal(a, ops.linear(x1, Wgu))
+    assert torch.equal(ops.decode_linear(act, Wd, residual=res), ops.linear(act, Wd, residual=res))
     z = x1.float() @ Wq.float().T
     y = ops.decode_linear(x1, Wq)
     assert (y.float() - z).abs().max().item() <= 8e-3 * z.abs().max().item()
