@@ -6,7 +6,7 @@
 // decode step appends one token and runs attn_decode: one query row per (batch, head) against
 // keys [kv_start[b], kv_len[b]). Decode attention is HBM-bound (every cached key and value is
 // read once per step), so it is split over the keys (flash-decoding): workgroup (chunk, h, b)
-// scores 128 keys with 8 lanes per key (each lane 16 dims, coalesced 256 B rows, all loads in
+// scores kChunk keys with 8 lanes per key (each lane 16 dims, coalesced 256 B rows, all loads in
 // flight before use), forms P.V with 16 dim-groups x 16 key-groups of 16 B loads, keeps the
 // chunk's max / sum / unnormalised P.V in f32 partials, and a combine kernel rescales and sums
 // the chunks in a fixed order (deterministic).
@@ -14,7 +14,9 @@
 
 namespace {
 
-constexpr int kChunk = 128;
+// keys per workgroup: 64 gives the batch-1 step 32 heads x 18 chunks = 576 workgroups at the
+// 1088-row prompt (128: 288, about one per CU, each waiting out a longer load ramp)
+constexpr int kChunk = 64;
 constexpr float kLog2e = 1.4426950408889634f;
 
 __global__ __launch_bounds__(256) void kv_append_k(const u16* __restrict__ ks, int64_t ldks, const u16* __restrict__ vs,
@@ -93,7 +95,7 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
       if (sub == 0) ps[pass * 32 + slot] = (key < kend && key >= k_lo) ? acc : -INFINITY;
     }
     __syncthreads();
-    // chunk max and sum (kChunk = 128 scores, threads >= 128 carry -inf / 0)
+    // chunk max and sum (kChunk scores, threads >= kChunk carry -inf / 0)
     const int lane = t & 63, wv = t >> 6;
     const float s = t < kChunk ? ps[t] : -INFINITY;
     float m = wave_max(s);
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
 
 // Combine: max over the chunks, then the rescaled sums in chunk order (deterministic). Up to
 // kCombineRegs chunks (max_len <= 2048) every partial is loaded before the first is used.
-constexpr int kCombineRegs = 16;
+constexpr int kCombineRegs = 2048 / kChunk;
 template <int D>
 __global__ __launch_bounds__(D) void attn_decode_combine_k(const float* __restrict__ part_o,
                                                           const float* __restrict__ part_ml, u16* __restrict__ O,
