@@ -373,17 +373,32 @@ __global__ __launch_bounds__(256) void adamw_k(T* __restrict__ p, const T* __res
   const float gs = gscale ? gscale[0] : 1.f;
   const float step_size = lr / bc1;
   const int64_t nvec = vec ? n / 8 : 0;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    float gv[8], pv[8], mv[8], vv[8];
-    load8(g + i * 8, gv);
-    load8(p + i * 8, pv);
-    load8(m + i * 8, mv);
-    load8(v + i * 8, vv);
+  // two grid-stride steps per trip: eight 16-B loads in flight per lane instead of four
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i0 = blockIdx.x * 256 + threadIdx.x; i0 < nvec; i0 += 2 * stride) {
+    float gv[2][8], pv[2][8], mv[2][8], vv[2][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) adamw_elem<T, S>(gv[j] * gs, pv[j], mv[j], vv[j], lr, b1, b2, eps, wd, bc2_sqrt, step_size);
-    store8(p + i * 8, pv);
-    store8(m + i * 8, mv);
-    store8(v + i * 8, vv);
+    for (int u = 0; u < 2; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < nvec) {
+        load8(g + i * 8, gv[u]);
+        load8(p + i * 8, pv[u]);
+        load8(m + i * 8, mv[u]);
+        load8(v + i * 8, vv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          adamw_elem<T, S>(gv[u][j] * gs, pv[u][j], mv[u][j], vv[u][j], lr, b1, b2, eps, wd, bc2_sqrt, step_size);
+        store8(p + i * 8, pv[u]);
+        store8(m + i * 8, mv[u]);
+        store8(v + i * 8, vv[u]);
+      }
+    }
   }
   for (int64_t i = nvec * 8 + blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float pv = Elt<T>::ld(p, i), mv = Elt<S>::ld(m, i), vv = Elt<S>::ld(v, i);
