@@ -1,7 +1,7 @@
 #!/bin/bash
 # closing pass at the round-4 head: every GPU test, smoke(), the default bench line
 set -o pipefail
-OUT=gpurun_out/r04x2
+OUT=gpurun_out/r04x3
 mkdir -p $OUT
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $OUT/gpu_tests.log | head -20; exit $rc; }
@@ -10,7 +10,7 @@ tail -1 $OUT/smoke.log
 timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
 python3 - <<'PY'
 import json
-d=json.loads(open('gpurun_out/r04x2/bench.json').read().strip().splitlines()[-1])
+d=json.loads(open('gpurun_out/r04x3/bench.json').read().strip().splitlines()[-1])
 print(d['metric'], d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['traffic'])
 for w,v in d.get('workloads',{}).items(): print(w, v.get('value'), v.get('ms_per_step'), (v.get('roofline') or {}).get('frac'), (v.get('roofline') or {}).get('traffic'))
 PY
