@@ -22,7 +22,12 @@ encoder, bs 64), config 5 (ViT-L + Llama-2-13B, L = 1600, bs 4) and the referenc
 config 3 (LoRA r=64 + projector / lm_head / embed, frozen base). They are reported under
 "workloads", each with its own roofline object; the headline (metric / value) stays config 3.
 
-Prints ONE JSON line on rank 0 (see README / DESIGN.md §Measurement for every field).
+Prints ONE compact JSON line on rank 0, the last line of stdout (<= 4 KiB, so a driver that keeps
+the tail of stdout always holds it whole): the headline, its roofline, the decoder-layer roofline,
+cpu_baseline, a one-line summary per sub-workload and (N > 1) the exchange. The full record (every
+GEMM family and shape with its library ceiling, each sub-workload's own full record) goes to the
+sidecar file --detail-out (default gpurun_out/bench_detail.json), named in the line's "detail".
+See README / DESIGN.md §Measurement for every field.
 """
 from __future__ import annotations
 
@@ -64,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--sub-workloads", default=",".join(SUB_WORKLOADS),
                     help="N=1 headline runs only: the other workloads timed in child processes ('' = none)")
     ap.add_argument("--no-sub", action="store_true", help="time this workload only")
+    ap.add_argument("--detail-out", default=os.path.join(REPO, "gpurun_out", "bench_detail.json"),
+                    help="sidecar file for the full record ('' = none); the stdout line stays compact")
     ap.add_argument("--launch-probe", action="store_true",
                     help="launcher self-test: form the world, all-reduce one tensor on the host, print one "
                          "JSON line on rank 0 (no GPU work; tests/test_bench_launch.py)")
@@ -93,9 +100,12 @@ def run_sub_workloads(args, names):
     """Each workload in its own child process (sequentially, before this process initialises the
     GPU), its one JSON line parsed and condensed; a failing child is reported, not fatal."""
     import subprocess
+    import tempfile
     out = {}
     for name in names:
-        cmd = [sys.executable, os.path.abspath(__file__), "--no-sub", "--no-cpu-baseline",
+        fd, side = tempfile.mkstemp(prefix=f"bench_{name}_", suffix=".json")
+        os.close(fd)
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-sub", "--no-cpu-baseline", "--detail-out", side,
                "--steps", str(min(args.steps, 10)), "--warmup", str(min(args.warmup, 3)), *SUB_WORKLOADS[name]]
         t0 = time.perf_counter()
         try:
@@ -104,16 +114,92 @@ def run_sub_workloads(args, names):
             if r.returncode != 0 or not lines:
                 out[name] = {"error": f"rc {r.returncode}: {(r.stderr or r.stdout)[-400:]}"}
                 continue
-            rec = json.loads(lines[-1])
+            try:
+                rec = json.load(open(side))  # the child's full record
+            except (OSError, ValueError):
+                rec = json.loads(lines[-1])
         except subprocess.TimeoutExpired:
             out[name] = {"error": "timed out after 600 s"}
             continue
-        keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops_per_gpu", "mfu",
-                "gflop_per_image", "loss", "roofline", "gemm_kernels", "gemm_shapes", "prefill_ms", "weight_bytes",
-                "step_roofline")
-        out[name] = {k: rec[k] for k in keep if k in rec}
-        out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        finally:
+            if os.path.exists(side):
+                os.remove(side)
+        rec.pop("detail", None)
+        rec["wall_s"] = round(time.perf_counter() - t0, 1)
+        out[name] = rec
     return out
+
+
+# ---- the compact headline line ----------------------------------------------------------------
+LINE_LIMIT = 4096  # bytes: the final stdout line must fit a driver's tail whole
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "model_tflops_per_gpu", "mfu", "loss", "gflop_per_image",
+             "prefill_ms")
+ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes", "mfma_busy",
+             "avg_ms", "launches_timed", "library_ceiling")
+
+
+def _short(s, n):
+    s = str(s)
+    return s if len(s) <= n else s[:n - 3] + "..."
+
+
+def workload_summary(rec: dict) -> dict:
+    """one sub-workload in a few fields: its value, step time and the frac of its roofline kernel"""
+    if "error" in rec:
+        return {"error": _short(rec["error"], 160)}
+    roof = rec.get("roofline") or {}
+    out = {"value": rec.get("value"), "unit": rec.get("unit"), "ms_per_step": rec.get("ms_per_step"),
+           "roofline_frac": roof.get("frac"), "bound": roof.get("bound"), "kernel": _short(roof.get("kernel", ""), 48)}
+    if "mfu" in rec:
+        out["mfu"] = rec["mfu"]
+    if "step_roofline" in rec:
+        out["step_roofline_frac"] = rec["step_roofline"].get("frac")
+    return out
+
+
+def compact_line(full: dict) -> dict:
+    """The final stdout line built from the full record: headline fields, the roofline without its
+    per-family tables, layer_roofline, cpu_baseline, exchange, one summary per sub-workload."""
+    line = {k: full[k] for k in HEAD_KEYS if k in full}
+    if isinstance(line.get("config"), dict) and "workload" in line["config"]:
+        line["config"] = dict(line["config"], workload=_short(line["config"]["workload"], 220))
+    roof = full.get("roofline") or {}
+    line["roofline"] = {k: roof[k] for k in ROOF_KEYS if k in roof}
+    if "kernel" in line["roofline"]:
+        line["roofline"]["kernel"] = _short(line["roofline"]["kernel"], 260)
+    for k in ("layer_roofline", "step_roofline", "exchange"):
+        if k in full:
+            line[k] = full[k]
+    if "cpu_baseline" in full:
+        cb = dict(full["cpu_baseline"])
+        cb["sample"] = _short(cb.get("sample", ""), 420)
+        line["cpu_baseline"] = cb
+    if "workloads" in full:
+        line["workloads"] = {n: workload_summary(r) for n, r in full["workloads"].items()}
+    if "detail" in full:
+        line["detail"] = full["detail"]
+    s = json.dumps(line)
+    if len(s.encode()) > LINE_LIMIT:  # never let the headline outgrow the tail: drop the optional parts
+        for k in ("workloads", "step_roofline", "data"):
+            line.pop(k, None)
+            if len(json.dumps(line).encode()) <= LINE_LIMIT:
+                break
+    return line
+
+
+def emit(full: dict, args) -> None:
+    """Full record to the sidecar (if any), then the compact line as the last line of stdout."""
+    path = getattr(args, "detail_out", "")
+    if path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            with open(path, "w") as f:
+                json.dump(full, f, indent=1)
+            full = dict(full, detail=os.path.relpath(os.path.abspath(path), REPO))
+        except OSError as e:
+            print(f"bench.py: could not write {path}: {e}", file=sys.stderr)
+    print(json.dumps(compact_line(full)), flush=True)
 
 
 
@@ -199,7 +285,7 @@ def vit_main(args):
             "gemm_shapes": gemm_shapes(launches, args.steps),
         }
         line["roofline"]["library_ceiling"] = line["gemm_kernels"][0]["library_ceiling"]
-        print(json.dumps(line), flush=True)
+        emit(line, args)
     if world > 1:
         dist.destroy_process_group()
 
@@ -293,7 +379,7 @@ def decode_main(args):
                           "achieved": round(wbytes / step_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                           "frac": round(wbytes / step_s / 8e12, 4)},
     }
-    print(json.dumps(line), flush=True)
+    emit(line, args)
 
 
 def cpu_baseline(cfg, text_len: int, budget_s: float):
@@ -375,6 +461,33 @@ def cpu_baseline(cfg, text_len: int, budget_s: float):
                        f"({t_lm:.2f}s) + 1 CLIP-L/14 layer fwd ({t_vit:.3f}s) + lm_head fwd+bwd ({t_head:.2f}s) at "
                        f"B=1, L={L}, extrapolated x{t.num_hidden_layers} LM / x{O.needed_vision_layers(ocfg, -2)} "
                        f"ViT layers; {time.perf_counter() - t_start:.1f}s of CPU work")}
+
+
+def layer_roofline(spans: dict, fl: dict, args, tc):
+    """The north star's "fused causal-attention + MLP step": one decoder layer (RMSNorm, q|k|v,
+    RoPE, causal flash attention, o_proj + residual, RMSNorm, gate|up, SwiGLU, down + residual;
+    reference cullavo/arch_cullavo.py:638-647 -> transformers LlamaDecoderLayer, FA2 per
+    load_cullavo.py:72) forward + backward, timed by HIP events on the compute stream around every
+    LlamaLayerFn forward and backward of the timed steps. Algorithmic FLOPs per layer and sample:
+    GEMM fwd 2·L·(4d² + 3dF) (x3 with dX + dW when the weights train, x2 when frozen) + causal
+    attention 2·L²·d (x3.5: forward + the FA2 backward's 2.5)."""
+    fwd, bwd = spans.get("fwd", []), spans.get("bwd", [])
+    if not fwd or not bwd:
+        return None
+    n_f, n_b = len(fwd), len(bwd)
+    ms_f, ms_b = sum(fwd) / n_f, sum(bwd) / n_b
+    gemm_mult = 3.0 if args.trainable == "full" else 2.0
+    per_sample = gemm_mult * fl["lm_gemm_layer"] + 3.5 * fl["lm_attn_layer"]
+    if args.trainable == "lora":  # the layer's own adapters (r = 64 on q, k, v, o, gate, up, down): fwd x3
+        from cullavo_amd.perf import _lora_fwd
+        d, f = tc.hidden_size, tc.intermediate_size
+        per_sample += 3 * _lora_fwd(args.text_len + 575, 64, [(d, d)] * 4 + [(f, d)] * 2 + [(d, f)])
+    flops = per_sample * args.batch
+    tf = flops / ((ms_f + ms_b) * 1e-3) / 1e12
+    return {"what": "one decoder layer fwd+bwd (attention + MLP + norms/RoPE/SwiGLU), HIP events per layer",
+            "fwd_ms": round(ms_f, 4), "bwd_ms": round(ms_b, 4), "layers_timed": min(n_f, n_b),
+            "gflop_per_layer": round(flops / 1e9, 1), "achieved": round(tf, 1), "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4)}
 
 
 def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
@@ -609,6 +722,8 @@ def main(argv=None):
     cfg = cm.config
     T = args.batch * (args.text_len + cfg.vision_config.num_patches - 1)
     ops.trace_gemm("all")
+    from cullavo_amd import functions as F
+    F.trace_layers(True)  # HIP events around every decoder layer's forward and backward
     reducer = tr.accel.reducer
     if reducer is not None:
         reducer.measure = True
@@ -624,6 +739,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     launches = ops.trace_launches()
+    spans = F.layer_spans()
     fams = gemm_families(launches)
     exchange = None
     if world > 1:
@@ -711,13 +827,16 @@ def main(argv=None):
             for f, entry in zip(fams[:6], line["gemm_kernels"]):
                 entry["library_ceiling"] = gemm_ceiling(f)
             line["roofline"]["library_ceiling"] = line["gemm_kernels"][0]["library_ceiling"]
+        lr = layer_roofline(spans, fl, args, cfg.text_config)
+        if lr is not None:
+            line["layer_roofline"] = lr
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, args.text_len, args.cpu_seconds)
         if subs is not None:
             line["workloads"] = subs
         if exchange is not None:
             line["exchange"] = exchange
-        print(json.dumps(line), flush=True)
+        emit(line, args)
     if world > 1:
         dist.destroy_process_group()
 

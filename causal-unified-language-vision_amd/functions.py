@@ -53,6 +53,46 @@ if DW_STREAM not in ("side", "off"):
     raise ValueError(f"CULLAVO_DW_STREAM={DW_STREAM!r}: expected side | off")
 _DW: dict = {}  # device -> {"stream": side stream, "main": stream to join, "queued": bool}
 
+# bench.py's layer roofline (the north star's "attention + MLP step"): HIP events on the compute
+# stream around every decoder layer's forward and backward; None = off
+_LAYER_EV: dict | None = None
+
+
+def trace_layers(on: bool) -> None:
+    """start (on) or stop recording LlamaLayerFn forward / backward spans"""
+    global _LAYER_EV
+    _LAYER_EV = {"fwd": [], "bwd": []} if on else None
+
+
+def layer_spans() -> dict:
+    """{"fwd": [ms, ...], "bwd": [ms, ...]} of the recorded layer spans (synchronises; stops tracing)"""
+    global _LAYER_EV
+    ev, _LAYER_EV = _LAYER_EV, None
+    out = {"fwd": [], "bwd": []}
+    if not ev:
+        return out
+    for k in out:
+        if ev[k]:
+            ev[k][-1][1].synchronize()
+        out[k] = [a.elapsed_time(b) for a, b in ev[k]]
+    return out
+
+
+def _span_begin():
+    if _LAYER_EV is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(torch.cuda.current_stream())
+    return e
+
+
+def _span_end(e0, kind: str) -> None:
+    if e0 is None or _LAYER_EV is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record(torch.cuda.current_stream())
+    _LAYER_EV[kind].append((e0, e1))
+
 
 def _dw_state(dev):
     st = _DW.get(dev)
@@ -156,6 +196,7 @@ class LlamaLayerFn(torch.autograd.Function):
         Fd = cfg.intermediate_size
         grad = _needs_grad(ctx)
         lg, tr, seed = layer.lora_groups, layer.training, sctx.lora_seed
+        span = _span_begin()
         x1, rstd1 = ops.rmsnorm_fwd(h, layer.input_layernorm.weight, cfg.rms_norm_eps)
         t, u_qkv = lg["qkv"].forward(x1, tr, seed)
         qkv = ops.linear(x1, layer.w_qkv(), addend=t)  # [T, 3d]: q | k | v
@@ -172,6 +213,7 @@ class LlamaLayerFn(torch.autograd.Function):
         t, u_d = lg["down"].forward(a, tr, seed)
         h3 = ops.linear(a, layer.mlp.down_proj.weight, residual=h2, addend=t)
         del t
+        _span_end(span, "fwd")
         if grad:
             ctx.layer, ctx.sctx, ctx.train = layer, sctx, tr
             ctx.saved = (h, x1, rstd1, qkv, o, lse, h2, x2, rstd2, gu, a, u_qkv, u_o, u_gu, u_d)
@@ -186,6 +228,7 @@ class LlamaLayerFn(torch.autograd.Function):
         lg, tr, seed = layer.lora_groups, ctx.train, sctx.lora_seed
         T, d = h.shape
         H, D = cfg.num_attention_heads, cfg.head_dim
+        span = _span_begin()
         dh3 = dh3.contiguous()
         # MLP. Without a LoRA adapter on down_proj the SwiGLU backward runs in the epilogue of
         # the down-projection dX GEMM (dh never stored); with one, dh collects the adapter's
@@ -231,6 +274,7 @@ class LlamaLayerFn(torch.autograd.Function):
         dw_in, beta_in = grad_slot(win) if trainable(win) else (None, 0.0)
         dh = ops.rmsnorm_bwd(dx1, h, win, rstd1, dres=dh2, dw=dw_in, beta=beta_in)
         commit(win)
+        _span_end(span, "bwd")
         return (dh, None, None) + (None,) * len(layer.fn_params())
 
 
