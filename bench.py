@@ -498,14 +498,12 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
     tile = _lib.lib().cullavo_gemm_plan(M, N, K, al, bl, ctypes.byref(g))
-    ldr = 0 if (al == 1 and os.environ.get("CULLAVO_GEMM_LOADERS") == "1") else 1  # gemm.hip default_ldr
     # the 256-row kernels' last template argument is the fused-LoRA flag (rocprofv3 prints it)
     lf = "true" if lora else "false"
-    names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 1: f"gemm256_k<{al}, {bl}, 1, 256, 128, 0, false>",
-             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, {ldr}, false>",
-             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, {ldr}, false> split-K + splitk_reduce_k<1>",
-             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, {ldr}, {lf}>", 12: f"gemmpp_k<{al}, {bl}, 1, 4>",
-             13: f"gemmpp_k<{al}, {bl}, 1, 5>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
+    names = {0: f"gemm_k<{al}, {bl}, 1, 0>",
+             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, 1, false>",
+             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false> split-K + splitk_reduce_k<1>",
+             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, 1, {lf}>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 

@@ -101,12 +101,6 @@ def lib():
             L.cullavo_gemm_set_group(int(os.environ["CULLAVO_GEMM_GROUP"]))
         if os.environ.get("CULLAVO_GEMM_DMA"):  # DMA-offset A/B (cullavo_gemm_set_dma)
             L.cullavo_gemm_set_dma(int(os.environ["CULLAVO_GEMM_DMA"]))
-        if os.environ.get("CULLAVO_GEMM_LOADERS"):  # dW loader-wave A/B (cullavo_gemm_set_loaders)
-            L.cullavo_gemm_set_loaders(int(os.environ["CULLAVO_GEMM_LOADERS"]))
-        if os.environ.get("CULLAVO_STREAMK"):  # stream-K tail A/B (cullavo_gemm_set_streamk)
-            L.cullavo_gemm_set_streamk(int(os.environ["CULLAVO_STREAMK"]))
-        if os.environ.get("CULLAVO_GEMM_PREFETCH"):  # L2 prefetch A/B (cullavo_gemm_set_prefetch)
-            L.cullavo_gemm_set_prefetch(int(os.environ["CULLAVO_GEMM_PREFETCH"]))
         if os.environ.get("CULLAVO_RATE288") is not None:  # 288-row tile A/B (0 = out of the plan)
             L.cullavo_gemm_set_tile_rate(10, float(os.environ["CULLAVO_RATE288"]), None)
         if os.environ.get("CULLAVO_ATTN_RESCALE"):  # deferred-rescale A/B (cullavo_attn_set_rescale)

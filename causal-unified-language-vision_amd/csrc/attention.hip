@@ -1621,728 +1621,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   }
 }
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq8_k(
-    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
-    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
-    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dQ,
-    int64_t lddq, int H, int Lq, int Lk, float scale, const int32_t* __restrict__ kv_start) {
-  constexpr int KT = 64;
-  constexpr int TILE = KT * D * 2;
-  constexpr int NS = D / 16;
-  constexpr int ND = D / 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nqb = (Lq + 127) / 128;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qi = lid % nqb, hb = lid / nqb;
-  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
-  const int h = hb % H, b = hb / H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
-  const int qsl = wave & 3, u = wave >> 2;  // 32-query slice, key half of each tile
-  const int q = qb * 128 + qsl * 32 + (lane & 31);
-  const int kstart = kv_start ? kv_start[b] : 0;
-
-  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
-  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
-  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
-  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
-
-  frag8 qf[NS], of[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const bool ok = q < Lq;
-    qf[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Qb + (int64_t)q * ldq + 16 * s + 8 * hf) : u16x8(0));
-    of[s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(dOb + (int64_t)q * lddo + 16 * s + 8 * hf) : u16x8(0));
-  }
-  const float lse2 = (q < Lq) ? LSE[((int64_t)b * H + h) * Lq + q] * kLog2e : INFINITY;
-  const float del = (q < Lq) ? DELTA[((int64_t)b * H + h) * Lq + q] : 0.f;
-  const float c = scale * kLog2e;
-  f32x16 dq[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i) dq[i] = f32x16(0.f);
-
-  int kend = Lk;
-  if (CAUSAL) kend = min(Lk, qb * 128 + 128);
-  const int ntiles = (kend + KT - 1) / KT;
-  const int t0 = kstart / KT;
-
-  StageN<KT, D, 512> sk, sv;
-  if (t0 < ntiles) {
-    sk.load(Kb, ldk, t0 * KT, Lk);
-    sv.load(Vb, ldv, t0 * KT, Lk);
-    sk.store(smem);
-    sv.store(smem + TILE);
-  }
-  __builtin_amdgcn_s_waitcnt(kVmcnt0);
-  __syncthreads();
-  for (int t = t0; t < ntiles; ++t) {
-    const int cur = (t - t0) & 1;
-    char* bK = smem + 2 * cur * TILE;
-    char* bV = bK + TILE;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      sk.load(Kb, ldk, (t + 1) * KT, Lk);
-      sv.load(Vb, ldv, (t + 1) * KT, Lk);
-    }
-    f32x16 st = f32x16(0.f), dpt = f32x16(0.f);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bK, 32 * u, s, lane), qf[s], st, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(bV, 32 * u, s, lane), of[s], dpt, 0, 0, 0);
-    }
-    const int kbase = t * KT + 32 * u;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kbase + acc_row(r, hf);
-      float pv = fast_exp2(fmaf(st[r], c, -lse2));
-      if (key >= Lk || key < kstart || (CAUSAL && key > q)) pv = 0.f;
-      dpt[r] = pv * (dpt[r] - del);
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const frag8 df = pack_frag(dpt, s);
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<D>(bK, 32 * u + 16 * s, dt * 32, lane), df, dq[dt], 0, 0, 0);
-    }
-    if (more) {
-      char* nK = smem + 2 * (cur ^ 1) * TILE;
-      sk.store(nK);
-      sv.store(nK + TILE);
-    }
-    __syncthreads();
-  }
-  // pair reduction (key half 1 -> LDS -> half 0 adds and stores)
-  float* red = (float*)smem;  // [4 slices][ND][16][64] f32
-  auto slot = [&](int dt, int r) { return red + (((qsl * ND + dt) * 16 + r) * 64 + lane); };
-  if (u == 1) {
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) *slot(dt, r) = dq[dt][r];
-  }
-  __syncthreads();
-  if (u == 0 && q < Lq) {
-    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        u16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = f2bf((dq[dt][rr * 4 + j] + *slot(dt, rr * 4 + j)) * scale);
-        *reinterpret_cast<u16x4*>(dQb + dt * 32 + 8 * rr + 4 * hf) = w;
-      }
-  }
-}
-
-// ============================================================================================
-// backward dK/dV, 64 keys per wave
-// ============================================================================================
-// One workgroup = 4 waves (one per SIMD, so up to 512 registers each) = 256 keys of one
-// (b, h). A wave keeps the K fragments of its 64 keys (two 32-key MFMA tiles) in registers,
-// their V rows in an LDS image and their dK / dV in 256 accumulator registers while the
-// workgroup sweeps 32-row Q / dO slices staged in LDS; every Q / dO row fragment and every
-// transposed fragment read from LDS feeds the MFMAs of both key tiles: 32 KiB of LDS reads
-// per 64 MFMAs per wave, against 48 KiB per 32 in the 8-wave kernel above, whose re-read K / V
-// rows made it LDS-bound (V in registers too spills at D = 128)
-// (cdna_hip_programming.md "Attention backward": key on the lane, dK / dV held in
-// accumulators over the whole sweep, no sum across workgroups).
-// Work order: key block kb = blockIdx / (B*H), so every (b, h)'s heaviest causal block (the
-// longest query sweep) is dispatched first and the one-block-per-CU rounds end together.
-// A wave whose 64 keys all lie after a slice's last query (causal diagonal) skips it.
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_w64_k(
-    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
-    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
-    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
-    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
-    const int32_t* __restrict__ kv_start) {
-  constexpr int QT = 32, KB = 256, J = 2;
-  constexpr int TQ = QT * D * 2;            // bytes of a Q (or dO) slice
-  constexpr int NS = D / 16;
-  constexpr int ND = D / 32;
-  constexpr int BUF = 2 * TQ + 2 * QT * 4;  // [Q | dO | lse*log2e (32) | delta (32)]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* sV = smem + 2 * BUF;                // V image of the block's 256 keys
-
-  const int nkb = (Lk + KB - 1) / KB;
-  const int BH = (int)gridDim.x / nkb;
-  const int kb = (int)blockIdx.x / BH, hb = (int)blockIdx.x % BH;
-  const int h = hb % H, b = hb / H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
-  const int kw = kb * KB + wave * 64;  // first key of this wave
-  const int kstart = kv_start ? kv_start[b] : 0;
-
-  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
-  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
-  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
-  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
-  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
-  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
-
-  frag8 kf[J][NS];
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const int key = kw + 32 * j + (lane & 31);
-    const bool ok = key < Lk;
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      kf[j][s] = __builtin_bit_cast(frag8, ok ? *reinterpret_cast<const u16x8*>(Kb + (int64_t)key * ldk + 16 * s + 8 * hf) : u16x8(0));
-  }
-  f32x16 dk[J][ND], dv[J][ND];
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-#pragma unroll
-    for (int i = 0; i < ND; ++i) { dk[j][i] = f32x16(0.f); dv[j][i] = f32x16(0.f); }
-  const float c = scale * kLog2e;
-
-  const int kmin = kb * KB;
-  const int qt0 = CAUSAL ? (kmin / QT) : 0;
-  const int nqt = (Lq + QT - 1) / QT;
-  const bool block_live = kmin < Lk && (kmin + KB > kstart);
-
-  StageN<QT, D, 256> sq, sdo;
-  float aux = 0.f;
-  // the next tile's lse / delta: loaded raw and first used when staged after the tile's compute
-  // (the lse * log2 e at load time made the compiler wait for the load -- and for the in-flight
-  // Q / dO prefetch -- at the top of every tile)
-  bool aux_in = false;
-  auto load_aux = [&](int qt) {
-    if (threadIdx.x < 2 * QT) {
-      const int qq = qt * QT + (int)threadIdx.x % QT;
-      aux_in = qq < Lq;
-      aux = (threadIdx.x < QT ? lseb : delb)[min(qq, Lq - 1)];
-    }
-  };
-  auto store_aux = [&](char* buf) {
-    if (threadIdx.x < 2 * QT)
-      ((float*)(buf + 2 * TQ))[threadIdx.x] =
-          threadIdx.x < QT ? (aux_in ? aux * kLog2e : INFINITY) : (aux_in ? aux : 0.f);
-  };
-  if (block_live) {
-#pragma unroll
-    for (int part = 0; part < KB / 64; ++part) {
-      StageN<64, D, 256> sv;
-      sv.load(Vb, ldv, kmin + 64 * part, Lk);
-      sv.store(sV + 64 * part * D * 2);
-    }
-  }
-  if (block_live && qt0 < nqt) {
-    sq.load(Qb, ldq, qt0 * QT, Lq);
-    sdo.load(dOb, lddo, qt0 * QT, Lq);
-    sq.store(smem);
-    sdo.store(smem + TQ);
-    load_aux(qt0);
-    store_aux(smem);
-  }
-  __builtin_amdgcn_s_waitcnt(kVmcnt0);  // see attn_fwd_k: keeps hipcc from waiting on the prefetch
-  __syncthreads();
-
-  // slices that end before this wave's first key (causal diagonal) only stage and sync: the
-  // same barrier count as the other waves, no branch around the MFMA body (a branch there
-  // makes hipcc spill the 256 accumulators' neighbours)
-  const int nq = block_live ? nqt : qt0;
-  const int qskip = CAUSAL ? min(nq, max(qt0, kw / QT)) : qt0;
-  int qt = qt0;
-  for (; qt < qskip; ++qt) {
-    char* nbuf = smem + ((qt - qt0 + 1) & 1) * BUF;
-    const bool more = qt + 1 < nqt;
-    if (more) {
-      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
-      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
-      load_aux(qt + 1);
-      sq.store(nbuf);
-      sdo.store(nbuf + TQ);
-      store_aux(nbuf);
-    }
-    __syncthreads();
-  }
-  for (; qt < nq; ++qt) {
-    const int cur = (qt - qt0) & 1;
-    char* buf = smem + cur * BUF;
-    char* nbuf = smem + (cur ^ 1) * BUF;
-    const bool more = qt + 1 < nqt;
-    if (more) {
-      sq.load(Qb, ldq, (qt + 1) * QT, Lq);
-      sdo.load(dOb, lddo, (qt + 1) * QT, Lq);
-      load_aux(qt + 1);
-    }
-    const int q0 = qt * QT;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));  // lane-derived LDS addresses: recomputed per slice, not hoisted
-    {
-      const float* slse = (const float*)(buf + 2 * TQ);
-      const float* sdel = slse + QT;
-      // S[q][key], dP[q][key] of both key tiles; one Q / dO row fragment per k-step
-      f32x16 sacc[J], pacc[J];
-#pragma unroll
-      for (int j = 0; j < J; ++j) { sacc[j] = f32x16(0.f); pacc[j] = f32x16(0.f); }
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const frag8 qa = row_frag<D>(buf, 0, s, ln);
-        const frag8 oa = row_frag<D>(buf + TQ, 0, s, ln);
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-          sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[j][s], sacc[j], 0, 0, 0);
-          pacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, row_frag<D>(sV, wave * 64 + 32 * j, s, ln), pacc[j], 0, 0, 0);
-        }
-      }
-      // P = exp2(S*c - lse*log2e), dS = P * (dP - delta); masks only where a bound crosses
-      const bool need_mask = (CAUSAL && kw + 63 > q0) || kw + 64 > Lk || kw < kstart || q0 + QT > Lq;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(slse + 8 * rr + 4 * hf);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(sdel + 8 * rr + 4 * hf);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int r = rr * 4 + jj;
-          const int qq = q0 + 8 * rr + 4 * hf + jj;
-#pragma unroll
-          for (int j = 0; j < J; ++j) {
-            float pv = fast_exp2(fmaf(sacc[j][r], c, -l4[jj]));
-            if (need_mask) {
-              const int key = kw + 32 * j + (lane & 31);
-              if ((CAUSAL && key > qq) || key < kstart || key >= Lk || qq >= Lq) pv = 0.f;
-            }
-            sacc[j][r] = pv;
-            pacc[j][r] = pv * (pacc[j][r] - d4[jj]);
-          }
-        }
-      }
-      // dV += P^T dO ; dK += dS^T Q: each transposed dO / Q fragment serves both key tiles
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        frag8 pf[J], df[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) { pf[j] = pack_frag(sacc[j], s); df[j] = pack_frag(pacc[j], s); }
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-          const frag8 tdo = tr_frag<D>(buf + TQ, 16 * s, dt * 32, ln);
-          const frag8 tq = tr_frag<D>(buf, 16 * s, dt * 32, ln);
-#pragma unroll
-          for (int j = 0; j < J; ++j) {
-            dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[j], tdo, dv[j][dt], 0, 0, 0);
-            dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df[j], tq, dk[j][dt], 0, 0, 0);
-          }
-        }
-      }
-    }
-    if (more) {
-      sq.store(nbuf);
-      sdo.store(nbuf + TQ);
-      store_aux(nbuf);
-    }
-    __syncthreads();
-  }
-
-  // dK/dV[key][d]: register r = key row, lane = d column
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = kw + 32 * j + acc_row(r, hf);
-        if (kk < Lk) {
-          const int d = dt * 32 + (lane & 31);
-          dK[((int64_t)b * Lk + kk) * lddk + (int64_t)h * D + d] = f2bf(dk[j][dt][r] * scale);
-          dV[((int64_t)b * Lk + kk) * lddv + (int64_t)h * D + d] = f2bf(dv[j][dt][r]);
-        }
-      }
-}
-
-// ============================================================================================
-// backward dK/dV, software-pipelined (mode 8)
-// ============================================================================================
-// One wave per SIMD: 4 waves, 128 keys per workgroup, each wave's 32 keys held as K and V row
-// fragments in registers (512 registers per wave leave room for them, for the 128 dK/dV
-// accumulators and for two tiles' S/dP), the workgroup sweeping 32-query Q / dO tiles through a
-// 3-slot LDS ring filled by LDS-DMA two tiles ahead (lse and delta ride along, 4 B per lane). Per
-// tile and wave (32 keys x 32 queries): S = Q K^T, dP = dO V^T (16 MFMAs), P = exp2(S c - lse),
-// dS = P (dP - delta) (VALU), dV += P^T dO, dK += dS^T Q (16 MFMAs). Iteration t runs tile t's
-// elementwise step in the issue gaps of tile t+1's S / dP MFMAs, then tile t's dV / dK MFMAs;
-// every LDS read is inline asm in counted groups (the next group in flight under the current
-// MFMAs). The elementwise arithmetic and the dS^T written for the dQ kernel are attn_bwd_dkdv8_k's
-// (bitwise); dK / dV sum a key's queries in sweep order (mode 7 adds two half-tile partials).
-template <int NR, unsigned OFF>
-DEV void rd128(s16x8 (&f)[NR], const unsigned (&a)[NR]) {
-#pragma unroll
-  for (int j = 0; j < NR; ++j) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[j]) : "v"(a[j]), "n"(OFF) : "memory");
-}
-template <int CNT, int NR>
-DEV void tie128(s16x8 (&f)[NR]) {
-#pragma unroll
-  for (int j = 0; j < NR; ++j) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[j]) : "n"(CNT) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-template <unsigned OFF>
-DEV void rdtr(s16x4& lo, s16x4& hi, unsigned alo, unsigned ahi) {
-  asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
-               : "=&v"(lo), "=&v"(hi) : "v"(alo), "v"(ahi), "n"(OFF) : "memory");
-}
-template <int CNT>
-DEV void tietr(s16x4& a, s16x4& b, s16x4& c, s16x4& d) {
-  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(CNT) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-DEV frag8 cat_tr(const s16x4& lo, const s16x4& hi) {
-  return __builtin_bit_cast(frag8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-DEV void lds_dma4(__amdgpu_buffer_rsrc_t rs, char* lds, unsigned vo) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 4, vo, 0, 0, 0);
-}
-
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_pipe_k(
-    const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ K, int64_t ldk,
-    const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
-    const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
-    int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
-    const int32_t* __restrict__ kv_start, u16* __restrict__ dST, int64_t ldst, int64_t st_bh) {
-  constexpr int QT = 32, KB = 128;
-  constexpr int TQ = QT * D * 2;      // bytes of a Q (or dO) tile image
-  constexpr int SLOT = 2 * TQ + 512;  // [Q | dO | lse(32, 256-B area) | delta(32, 256-B area)]
-  constexpr int NS = D / 16;
-  constexpr int ND = D / 32;
-  constexpr int NG = NS / 2;          // S / dP groups: 2 k-steps = 4 MFMAs each
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nkb = (Lk + KB - 1) / KB;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int kb = lid % nkb, hb = lid / nkb;
-  const int h = hb % H, b = hb / H;
-  const int lane = threadIdx.x & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int k0 = kb * KB + 32 * wave;
-  const int key = k0 + (lane & 31);
-  const int kstart = kv_start ? kv_start[b] : 0;
-  const int qlo = CAUSAL ? key : 0;
-  const int qlim = (key < kstart || key >= Lk) ? qlo : Lq;
-  const unsigned qspan = (unsigned)max(qlim - qlo, 0);
-
-  const u16* Qb = Q + (int64_t)b * Lq * ldq + (int64_t)h * D;
-  const u16* dOb = dO + (int64_t)b * Lq * lddo + (int64_t)h * D;
-  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
-  const u16* Vb = V + (int64_t)b * Lk * ldv + (int64_t)h * D;
-  const float* lseb = LSE + ((int64_t)b * H + h) * Lq;
-  const float* delb = DELTA + ((int64_t)b * H + h) * Lq;
-
-  frag8 kf[NS], vf[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const bool in = key < Lk;
-    kf[s] = __builtin_bit_cast(frag8, in ? *reinterpret_cast<const u16x8*>(Kb + (int64_t)key * ldk + 16 * s + 8 * hf) : u16x8(0));
-    vf[s] = __builtin_bit_cast(frag8, in ? *reinterpret_cast<const u16x8*>(Vb + (int64_t)key * ldv + 16 * s + 8 * hf) : u16x8(0));
-  }
-  f32x16 dk[ND], dv[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i) { dk[i] = f32x16(0.f); dv[i] = f32x16(0.f); }
-  const float c = scale * kLog2e;
-  const int kmin = kb * KB;
-  const int qt0 = CAUSAL ? (kmin / QT) : 0;
-  const int nqt = (Lq + QT - 1) / QT;
-  const bool block_live = kmin < Lk && (kmin + KB > kstart);
-
-  StageDMA1<QT, D, 4> dq_, ddo_;
-  dq_.prep(ldq, wave, lane);
-  ddo_.prep(lddo, wave, lane);
-  // tile t into slot sl: Q, dO images (every wave its pieces), lse / delta (wave 0, one 4-byte
-  // LDS-DMA each by waves 0 / 1; rows past Lq land as zeros and are masked)
-  auto dma = [&](int t, int sl) {
-    char* base = smem + sl * SLOT;
-    dq_.issue(Qb, ldq, t * QT, Lq, base, wave);
-    ddo_.issue(dOb, lddo, t * QT, Lq, base + TQ, wave);
-    if (wave < 2) {
-      // lse (wave 0) / delta (wave 1): 64 lanes x 4 B into a 256-B area each, rows past the tile
-      // or Lq outside the descriptor's range (zeros)
-      const int left = min(Lq - t * QT, QT);
-      const int bytes = left > 0 ? left * 4 : 0;
-      const float* src = (wave == 0 ? lseb : delb) + t * QT;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, bytes, 0x00020000);
-      lds_dma4(rs, base + 2 * TQ + 256 * wave, (unsigned)(lane * 4));
-    }
-  };
-
-  // per-lane LDS byte offsets within a slot: Q / dO row fragments (A operands of S / dP; dO at
-  // +TQ), their transposed fragments (B operands of dV / dK, 16-query half s at +16 s rows), and
-  // this lane's four lse / delta quads (query rows 8 rr + 4 hf + 0..3)
-  const unsigned sbase = lds_addr(smem);
-  unsigned roff[NS];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) roff[s] = kv_off<D>(lane & 31, 2 * s + hf);
-  unsigned toff[ND][2];
-  {
-    const int i = lane & 15, qq = i >> 2, p = i & 3;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt) {
-      const int ch = ((dt * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
-      toff[dt][0] = kv_off<D>(4 * hf + qq, ch) + 8 * (p & 1);
-      toff[dt][1] = kv_off<D>(4 * hf + qq + 8, ch) + 8 * (p & 1);
-    }
-  }
-  const unsigned laux = 2 * TQ + 16 * hf;  // + 32 rr bytes; delta at + 256
-
-  u16* dsrow = dST + ((int64_t)b * H + h) * st_bh + (int64_t)key * ldst + 4 * hf;
-
-  // S / dP of the tile in slot base sb (bytes), plain (prologue)
-  auto sdp_plain = [&](unsigned sb, f32x16& sa, f32x16& pa) {
-    sa = f32x16(0.f);
-    pa = f32x16(0.f);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(sbase + sb + roff[s]), kf[s], sa, 0, 0, 0);
-      pa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lds_frag(sbase + sb + TQ + roff[s]), vf[s], pa, 0, 0, 0);
-    }
-  };
-
-  // iteration t: sc / pc hold tile t's S / dP (slot base cb); NEXT: tile t+1's S / dP (slot nb)
-  // into sn / pn beside tile t's elementwise step; then tile t's dV / dK
-  auto iter = [&](auto next_c, int t, unsigned cb, unsigned nb, f32x16& sc, f32x16& pc, f32x16& sn, f32x16& pn) {
-    constexpr bool NEXT = decltype(next_c)::value;
-    // mask (tiles crossing the causal diagonal of this wave's keys, the sequence end, kv_start)
-    const bool need_mask = (CAUSAL && t * QT < k0 + 32) || t * QT + QT > Lq || k0 < kstart || k0 + 32 > Lk;
-    if (need_mask) {
-      const int qoff = t * QT + 4 * hf - qlo;
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        sc[r] = (unsigned)(qoff + acc_row(r, 0)) >= qspan ? -INFINITY : sc[r];
-    }
-    // lse / delta quads of tile t, two per elementwise chunk, issued one group ahead of their chunk
-    // beside the fragment reads (few registers in flight: under register pressure the compiler
-    // parks long-lived asm outputs in AGPRs, copying them before the data has landed)
-    s16x8 auxa[2], auxb[2];
-    auto aux_issue = [&](auto rr_c, s16x8 (&f)[2]) {
-      constexpr int RR = decltype(rr_c)::value;
-      const unsigned a0 = sbase + cb + laux + 32 * RR;
-      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[0]) : "v"(a0) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:256" : "=&v"(f[1]) : "v"(a0) : "memory");
-    };
-    s16x8 ga[4], gb[4];
-    auto issue = [&](auto g_c, s16x8 (&f)[4]) {
-      constexpr int G = decltype(g_c)::value;
-      unsigned a[4] = {sbase + nb + roff[2 * G], sbase + nb + roff[2 * G], sbase + nb + roff[2 * G + 1],
-                       sbase + nb + roff[2 * G + 1]};
-      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[0]) : "v"(a[0]) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[1]) : "v"(a[1]), "n"(TQ) : "memory");
-      asm volatile("ds_read_b128 %0, %1" : "=&v"(f[2]) : "v"(a[2]) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=&v"(f[3]) : "v"(a[3]), "n"(TQ) : "memory");
-    };
-    auto mm = [&](auto g_c, s16x8 (&f)[4]) {
-      constexpr int G = decltype(g_c)::value;
-      sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[0]), kf[2 * G], sn, 0, 0, 0);
-      pn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[1]), vf[2 * G], pn, 0, 0, 0);
-      sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[2]), kf[2 * G + 1], sn, 0, 0, 0);
-      pn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, f[3]), vf[2 * G + 1], pn, 0, 0, 0);
-    };
-    frag8 pf[2], df[2];
-    // elementwise chunk rr: accumulator registers 4 rr .. 4 rr + 3 (query rows 8 rr + 4 hf + 0..3)
-    auto chunk = [&](auto rr_c) {
-      constexpr int RR = decltype(rr_c)::value;
-      // the quads are valid only after the group's counted wait, which ties them (no pins on the
-      // S / dP accumulators: an asm operand would move them out of AGPRs)
-      s16x8 (&ax)[2] = RR % 2 == 0 ? auxa : auxb;
-      const f32x4 l4 = __builtin_bit_cast(f32x4, ax[0]);
-      const f32x4 d4 = __builtin_bit_cast(f32x4, ax[1]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = RR * 4 + j;
-        const float pv = fast_exp2(fmaf(sc[r], c, -(l4[j] * kLog2e)));
-        sc[r] = pv;
-        pc[r] = pv * (pc[r] - d4[j]);
-      }
-      if constexpr (RR % 2 == 1) {
-        constexpr int S = RR / 2;
-        pf[S] = pack_frag(sc, S);
-        df[S] = pack_frag(pc, S);
-        const u16x8 w = __builtin_bit_cast(u16x8, df[S]);
-        u16* row = dsrow + t * QT + 16 * S;
-        *reinterpret_cast<u16x4*>(row) = u16x4{w[0], w[1], w[2], w[3]};
-        *reinterpret_cast<u16x4*>(row + 8) = u16x4{w[4], w[5], w[6], w[7]};
-        pin(pf[S]);
-        pin(df[S]);
-      }
-    };
-    // waits: group g's 4 fragments and chunk g's 2 quads; the next group's 6 reads stay in flight
-    auto tie6 = [&](auto cnt_c, s16x8 (&f)[4], s16x8 (&ax)[2]) {
-      constexpr int CNT = decltype(cnt_c)::value;
-      asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(ax[0]), "+v"(ax[1])
-                   : "n"(CNT) : "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    using C0 = std::integral_constant<int, 0>;
-    using C1 = std::integral_constant<int, 1>;
-    using C2 = std::integral_constant<int, 2>;
-    using C3 = std::integral_constant<int, 3>;
-    using W6 = std::integral_constant<int, 6>;
-    using W0 = std::integral_constant<int, 0>;
-    if constexpr (NEXT && NG == 4) {
-      sn = f32x16(0.f);
-      pn = f32x16(0.f);
-      aux_issue(C0{}, auxa);
-      issue(C0{}, ga);
-      aux_issue(C1{}, auxb);
-      issue(C1{}, gb);
-      tie6(W6{}, ga, auxa);
-      mm(C0{}, ga);
-      chunk(C0{});
-      interleave<4, 5>();
-      aux_issue(C2{}, auxa);
-      issue(C2{}, ga);
-      tie6(W6{}, gb, auxb);
-      mm(C1{}, gb);
-      chunk(C1{});
-      interleave<4, 9>();
-      aux_issue(C3{}, auxb);
-      issue(C3{}, gb);
-      tie6(W6{}, ga, auxa);
-      mm(C2{}, ga);
-      chunk(C2{});
-      interleave<4, 5>();
-      tie6(W0{}, gb, auxb);
-      mm(C3{}, gb);
-      chunk(C3{});
-      interleave<4, 9>();
-    } else if constexpr (NEXT) {  // D = 64: two groups of 4 MFMAs, chunks 2 and 3 after them
-      sn = f32x16(0.f);
-      pn = f32x16(0.f);
-      aux_issue(C0{}, auxa);
-      issue(C0{}, ga);
-      aux_issue(C1{}, auxb);
-      issue(C1{}, gb);
-      tie6(W6{}, ga, auxa);
-      mm(C0{}, ga);
-      chunk(C0{});
-      interleave<4, 5>();
-      aux_issue(C2{}, auxa);
-      tie6(std::integral_constant<int, 2>{}, gb, auxb);
-      mm(C1{}, gb);
-      chunk(C1{});
-      interleave<4, 9>();
-      aux_issue(C3{}, auxb);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
-      chunk(C2{});
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
-      chunk(C3{});
-    } else {
-      aux_issue(C0{}, auxa);
-      aux_issue(C1{}, auxb);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
-      chunk(C0{});
-      aux_issue(C2{}, auxa);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
-      chunk(C1{});
-      aux_issue(C3{}, auxb);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(auxa[0]), "+v"(auxa[1]) :: "memory");
-      chunk(C2{});
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(auxb[0]), "+v"(auxb[1]) :: "memory");
-      chunk(C3{});
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // dV += P^T dO, dK += dS^T Q over tile t (slot cb): per (half s, column block dt) the dO and Q
-    // transposed fragments (4 tr reads), one group ahead
-    s16x4 ta[4], tb[4];
-    auto tiss = [&](auto i_c, s16x4 (&f)[4]) {
-      constexpr int I = decltype(i_c)::value;
-      constexpr int S = I / ND, DT = I % ND;
-      constexpr unsigned RO = 16 * S * 2 * D;
-      rdtr<TQ + RO>(f[0], f[1], sbase + cb + toff[DT][0], sbase + cb + toff[DT][1]);
-      rdtr<RO>(f[2], f[3], sbase + cb + toff[DT][0], sbase + cb + toff[DT][1]);
-    };
-    auto tmm = [&](auto i_c, s16x4 (&f)[4]) {
-      constexpr int I = decltype(i_c)::value;
-      constexpr int S = I / ND, DT = I % ND;
-      dv[DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[S], cat_tr(f[0], f[1]), dv[DT], 0, 0, 0);
-      dk[DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df[S], cat_tr(f[2], f[3]), dk[DT], 0, 0, 0);
-    };
-    constexpr int NI = 2 * ND;
-    tiss(std::integral_constant<int, 0>{}, ta);
-    tiss(std::integral_constant<int, 1>{}, tb);
-    auto tstep = [&](auto i_c) {
-      constexpr int I = decltype(i_c)::value;
-      if constexpr (I % 2 == 0) {
-        tietr<I + 1 < NI ? 4 : 0>(ta[0], ta[1], ta[2], ta[3]);
-        tmm(i_c, ta);
-        if constexpr (I + 2 < NI) tiss(std::integral_constant<int, I + 2>{}, ta);
-      } else {
-        tietr<I + 1 < NI ? 4 : 0>(tb[0], tb[1], tb[2], tb[3]);
-        tmm(i_c, tb);
-        if constexpr (I + 2 < NI) tiss(std::integral_constant<int, I + 2>{}, tb);
-      }
-    };
-    tstep(std::integral_constant<int, 0>{});
-    tstep(std::integral_constant<int, 1>{});
-    tstep(std::integral_constant<int, 2>{});
-    tstep(std::integral_constant<int, 3>{});
-    if constexpr (NI > 4) {
-      tstep(std::integral_constant<int, 4 % NI>{});
-      tstep(std::integral_constant<int, 5 % NI>{});
-      tstep(std::integral_constant<int, 6 % NI>{});
-      tstep(std::integral_constant<int, 7 % NI>{});
-    }
-    if constexpr (NEXT) {
-      // tile t+2 landed; every wave's reads of slot cb (refilled next iteration) are done
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  };
-
-  if (block_live && qt0 < nqt) {
-    dma(qt0, 0);
-    if (qt0 + 1 < nqt) dma(qt0 + 1, 1);
-    __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    __syncthreads();
-    f32x16 sa, pa, sb2, pb2;
-    sdp_plain(0, sa, pa);
-    using NT = std::integral_constant<bool, true>;
-    using NF = std::integral_constant<bool, false>;
-    // slots rotate 0 -> 1 -> 2; iteration t refills slot (t - qt0 + 2) % 3 with tile t + 2
-    int t = qt0;
-    unsigned cs = 0, ns = 1;  // slot of tile t, of tile t + 1
-    auto step = [&](auto next_c, f32x16& sc, f32x16& pc, f32x16& sn, f32x16& pn) {
-      const unsigned fs = 3 - cs - ns;  // the third slot
-      if constexpr (decltype(next_c)::value) {
-        if (t + 2 < nqt) dma(t + 2, (int)fs);
-      }
-      iter(next_c, t, cs * SLOT, ns * SLOT, sc, pc, sn, pn);
-      cs = ns;
-      ns = fs;
-      ++t;
-    };
-    for (; t + 2 < nqt;) {
-      step(NT{}, sa, pa, sb2, pb2);
-      step(NT{}, sb2, pb2, sa, pa);
-    }
-    if (t + 1 < nqt) {
-      step(NT{}, sa, pa, sb2, pb2);
-      step(NF{}, sb2, pb2, sa, pa);
-    } else {
-      step(NF{}, sa, pa, sb2, pb2);
-    }
-  }
-
-  // dK (x scale) and dV of this wave's 32 keys: lane column d = 32 dt + (lane & 31), rows
-  // acc_row(r, hf) (scalar row offsets, one 32-bit lane offset, as attn_bwd_dkdv8_k)
-  u16* dKr = dK + ((int64_t)b * Lk + k0) * lddk + (int64_t)h * D;
-  u16* dVr = dV + ((int64_t)b * Lk + k0) * lddv + (int64_t)h * D;
-  const unsigned lk = (unsigned)(4 * hf * lddk + (lane & 31)) * 2u, lv = (unsigned)(4 * hf * lddv + (lane & 31)) * 2u;
-  const int left = Lk - k0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    if (acc_row(r, hf) < left) {
-      u16* pk = dKr + (int64_t)acc_row(r, 0) * lddk;
-      u16* pv = dVr + (int64_t)acc_row(r, 0) * lddv;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt) {
-        *(u16*)((char*)pk + (lk + dt * 64u)) = f2bf(dk[dt][r] * scale);
-        *(u16*)((char*)pv + (lv + dt * 64u)) = f2bf(dv[dt][r]);
-      }
-    }
-  }
-}
-
 // ============================================================================================
 // backward dQ from the stored dS (mode 7)
 // ============================================================================================
@@ -2469,133 +1747,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
   }
 }
 
-// dQ from the stored dS, streaming form (mode 8): the kernel above reads its 0.3 GB of dS^T (7B
-// layer) with one tile of lookahead and a vmcnt(0) per tile, so every tile waits out an HBM
-// round trip (2.5 TB/s). Here a 3-slot ring (K tile + dS^T tile per slot, 96 KiB, one 8-wave
-// workgroup per CU) keeps two tiles in flight by LDS-DMA with a counted vmcnt, and the transposed
-// fragment reads are inline asm (the builtin would make hipcc wait for every in-flight DMA). Wave
-// w: queries 32 (w & 3) of the 128-query block, the D-half w >> 2 of dQ. Same products in the same
-// order per output as attn_bwd_dq_ds_k (bitwise equal).
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq_ds3_k(const u16* __restrict__ K, int64_t ldk,
-                                                            const u16* __restrict__ dST, int64_t ldst, int64_t st_bh,
-                                                            int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
-                                                            int Lq, int Lk, float scale,
-                                                            const int32_t* __restrict__ kv_start) {
-  constexpr int KT = 64, QB = 128;
-  constexpr int TK = KT * D * 2, TS = KT * QB * 2, SL = TK + TS;
-  constexpr int NS = KT / 16, ND = D / 32, NDW = ND / 2;  // k-steps per tile, dt per wave
-  constexpr int NPW = StageDMA1<KT, D, 8>::kPer + StageDMA1<KT, QB, 8>::kPer;  // DMA instrs per tile per wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nqb = (Lq + QB - 1) / QB;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int qi = lid % nqb, hb = lid / nqb;
-  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
-  const int h = hb % H, b = hb / H;
-  const int lane = threadIdx.x & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int qw = wave & 3, dh = wave >> 2;
-  const int q = qb * QB + qw * 32 + (lane & 31);
-  const int kstart = kv_start ? kv_start[b] : 0;
-  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
-  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * QB;
-
-  f32x16 dq[NDW];
-#pragma unroll
-  for (int i = 0; i < NDW; ++i) dq[i] = f32x16(0.f);
-  int kend = Lk;
-  if (CAUSAL) kend = min(Lk, qb * QB + QB);
-  const int ntiles = (kend + KT - 1) / KT;
-  const int t0 = kstart / KT;
-
-  StageDMA1<KT, D, 8> dk_;
-  StageDMA1<KT, QB, 8> ds_;
-  dk_.prep(ldk, wave, lane);
-  ds_.prep(ldst, wave, lane);
-  auto dma = [&](int t, int sl) {
-    dk_.issue(Kb, ldk, t * KT, Lk, smem + sl * SL, wave);
-    ds_.issue(Sb, ldst, t * KT, LkP, smem + sl * SL + TK, wave);
-  };
-  // per-lane transposed-fragment offsets (k-step 0; k-step s at + 32 W s): K^T columns of this
-  // wave's dt blocks, dS^T columns of its 32 queries
-  const unsigned sbase = lds_addr(smem);
-  unsigned ko[NDW][2], so[2];
-  {
-    const int i = lane & 15, qq = i >> 2, p = i & 3;
-    const int r0 = 4 * hf + qq;
-#pragma unroll
-    for (int j = 0; j < NDW; ++j) {
-      const int ch = (((dh * NDW + j) * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
-      ko[j][0] = sbase + kv_off<D>(r0, ch) + 8 * (p & 1);
-      ko[j][1] = sbase + kv_off<D>(r0 + 8, ch) + 8 * (p & 1);
-    }
-    const int ch = ((qw * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
-    so[0] = sbase + TK + kv_off<QB>(r0, ch) + 8 * (p & 1);
-    so[1] = sbase + TK + kv_off<QB>(r0 + 8, ch) + 8 * (p & 1);
-  }
-  // k-step S of the tile in slot base sb: its dS^T fragment and this wave's K^T fragments
-  auto rd = [&](auto s_c, unsigned sb, s16x4 (&f)[2 + 2 * NDW]) {
-    constexpr int S = decltype(s_c)::value;
-    rdtr<S * 32 * QB>(f[0], f[1], so[0] + sb, so[1] + sb);
-#pragma unroll
-    for (int j = 0; j < NDW; ++j) rdtr<S * 32 * D>(f[2 + 2 * j], f[3 + 2 * j], ko[j][0] + sb, ko[j][1] + sb);
-  };
-  auto tie = [&](auto cnt_c, s16x4 (&f)[2 + 2 * NDW]) {
-    constexpr int CNT = decltype(cnt_c)::value;
-#pragma unroll
-    for (int j = 0; j < 2 + 2 * NDW; ++j) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(f[j]) : "n"(CNT) : "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mm = [&](s16x4 (&f)[2 + 2 * NDW]) {
-    const frag8 bs = cat_tr(f[0], f[1]);
-#pragma unroll
-    for (int j = 0; j < NDW; ++j)
-      dq[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cat_tr(f[2 + 2 * j], f[3 + 2 * j]), bs, dq[j], 0, 0, 0);
-  };
-  constexpr int NR = 2 + 2 * NDW;  // tr reads per k-step
-
-  if (t0 < ntiles) {
-    dma(t0, 0);
-    if (t0 + 1 < ntiles) dma(t0 + 1, 1);
-    int sl = 0;
-    for (int t = t0; t < ntiles; ++t) {
-      // tile t landed (tile t+1 may stay in flight), every wave is done with slot (t-1) % 3
-      if (t + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + 2 < ntiles) dma(t + 2, sl == 0 ? 2 : sl - 1);
-      const unsigned sb = (unsigned)(sl * SL);
-      s16x4 fa[NR], fb[NR];
-      rd(std::integral_constant<int, 0>{}, sb, fa);
-      rd(std::integral_constant<int, 1>{}, sb, fb);
-      tie(std::integral_constant<int, NR>{}, fa);
-      mm(fa);
-      rd(std::integral_constant<int, 2>{}, sb, fa);
-      tie(std::integral_constant<int, NR>{}, fb);
-      mm(fb);
-      rd(std::integral_constant<int, 3>{}, sb, fb);
-      tie(std::integral_constant<int, NR>{}, fa);
-      mm(fa);
-      tie(std::integral_constant<int, 0>{}, fb);
-      mm(fb);
-      sl = sl == 2 ? 0 : sl + 1;
-    }
-  }
-  if (q < Lq) {
-    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
-#pragma unroll
-    for (int j = 0; j < NDW; ++j)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        u16x4 w;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = f2bf(dq[j][rr * 4 + e] * scale);
-        *reinterpret_cast<u16x4*>(dQb + (dh * NDW + j) * 32 + 8 * rr + 4 * hf) = w;
-      }
-  }
-}
-
 int64_t ds_rows(int Lk) { return cdiv(Lk, 128) * 128; }
 int64_t ds_cols(int Lq) { return cdiv(Lq, 128) * 128; }
 
@@ -2666,9 +1817,10 @@ int bwd_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* 
   return cullavo_check_launch("attn_bwd");
 }
 
-// DQ8: the 8-wave dQ kernel; else the 4-wave dQ kernel with 32-key tiles (measured faster
-// in the 7B step: 251 vs 284 us per layer, the dQ sweep has half the MFMAs per tile)
-template <int D, bool CAUSAL, bool DQ8>
+// mode 4: the 8-wave dK/dV kernel + the 4-wave dQ kernel with 32-key tiles (the recompute path
+// when no dS^T workspace is given; the 8-wave dQ kernel, mode 5, measured slower: 284 vs 251 us per
+// 7B layer, and was removed in round 5)
+template <int D, bool CAUSAL>
 int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
                 int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
                 u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
@@ -2678,13 +1830,12 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
   // dK/dV: K, V images (2 x 128 x D) + 2 x [Q | dO | lse | delta] tiles of 64 rows; the pair
   // reduction reuses the front 2 x 4 x 32 x D f32 of it
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
-  const int smem_b = DQ8 ? std::max(4 * 64 * D * 2, 4 * 32 * D * 4) : 4 * 32 * D * 2;
+  const int smem_b = 4 * 32 * D * 2;
   static bool once = false;
   if (!once) {
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL>, smem_a);
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, false, true>, smem_a);
-    if (DQ8) set_smem(attn_bwd_dq8_k<D, CAUSAL>, smem_b);
-    else set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
+    set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
     once = true;
   }
   if (g_bwd_stage & 1)
@@ -2693,12 +1844,8 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
   else
     attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
-  if (DQ8)
-    attn_bwd_dq8_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_b, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
-  else
-    attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
+  attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
+      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
@@ -2707,12 +1854,10 @@ template <int D, bool CAUSAL>
 int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
                   int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
                   u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
-                  const int32_t* ks, u16* ds, hipStream_t s, bool pipe = false) {
+                  const int32_t* ks, u16* ds, hipStream_t s) {
   const int64_t rows = (int64_t)B * Lq * H;
   attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
-  const int smem_p = 3 * (2 * 32 * D * 2 + 512);
-  const int smem_q = 3 * (64 * D * 2 + 64 * 128 * 2);
   const int smem_b = 2 * (64 * D * 2 + 64 * 128 * 2);
   static bool once = false;
   if (!once) {
@@ -2720,24 +1865,16 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true, true>, smem_a);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL, true>, smem_b);
-    set_smem(attn_bwd_dkdv_pipe_k<D, CAUSAL>, smem_p);
-    set_smem(attn_bwd_dq_ds3_k<D, CAUSAL>, smem_q);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
-  if (pipe)
-    attn_bwd_dkdv_pipe_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 256, smem_p, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
-  else if (g_bwd_stage & 1)
+  if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, true, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
   else
     attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
         q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
-  if (pipe)
-    attn_bwd_dq_ds3_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 512, smem_q, s>>>(
-        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
-  else if (g_bwd_stage & 2)
+  if (g_bwd_stage & 2)
     attn_bwd_dq_ds_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
         k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   else
@@ -2746,29 +1883,6 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
   return cullavo_check_launch("attn_bwd");
 }
 
-
-// mode 6: the 64-keys-per-wave dK/dV kernel + the 4-wave 32-key dQ kernel
-template <int D, bool CAUSAL>
-int bwd64_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16* v, int64_t ldv, const u16* o,
-                 int64_t ldo, const u16* dout, int64_t lddo, const float* lse, float* delta, u16* dq, int64_t lddq,
-                 u16* dk, int64_t lddk, u16* dv, int64_t lddv, int B, int H, int Lq, int Lk, float scale,
-                 const int32_t* ks, hipStream_t s) {
-  const int64_t rows = (int64_t)B * Lq * H;
-  attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
-  const int smem_a = 2 * (2 * 32 * D * 2 + 2 * 32 * 4) + 256 * D * 2;
-  const int smem_b = 4 * 32 * D * 2;
-  static bool once = false;
-  if (!once) {
-    set_smem(attn_bwd_dkdv_w64_k<D, CAUSAL>, smem_a);
-    set_smem(attn_bwd_dq_k<D, CAUSAL, 32>, smem_b);
-    once = true;
-  }
-  attn_bwd_dkdv_w64_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 256) * H * B), 256, smem_a, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks);
-  attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
-      q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
-  return cullavo_check_launch("attn_bwd");
-}
 
 // backward tile shape (cullavo_attn_set_bwd_tiles): bit 0 -> 64 query rows per dK/dV
 // barrier, bit 1 -> 64 keys per dQ barrier (else 32); -1 = per head dim, from the MI355X
@@ -2799,7 +1913,7 @@ extern "C" int cullavo_attn_set_rescale(float threshold, float* previous) {
 
 extern "C" int cullavo_attn_set_bwd_tiles(int mode) {
   const int prev = g_bwd_tiles;
-  if (mode >= -1 && mode <= 8) g_bwd_tiles = mode;
+  if ((mode >= -1 && mode <= 4) || mode == 7) g_bwd_tiles = mode;
   return prev;
 }
 
@@ -2832,7 +1946,7 @@ extern "C" int cullavo_attn_fwd(const void* q, int64_t ldq, const void* k, int64
 static int bwd_mode(int D) { return g_bwd_tiles >= 0 ? g_bwd_tiles : (D == 128 ? 7 : 2); }
 
 extern "C" size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype) {
-  if (dtype != CULLAVO_DT_BF16 || D < 64 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (bwd_mode(D) != 7 && bwd_mode(D) != 8))
+  if (dtype != CULLAVO_DT_BF16 || D < 64 || B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || (bwd_mode(D) != 7))
     return 0;
   return (size_t)B * H * ds_rows(Lk) * ds_cols(Lq) * 2;
 }
@@ -2874,31 +1988,20 @@ extern "C" int cullavo_attn_bwd_ws(const void* q, int64_t ldq, const void* k, in
   // B=64, T=577, H=16): there the 4-wave kernels already hold K/V in registers at < 256
   // VGPRs and the 8-wave LDS re-reads cost more than the second wave hides (tools/attn_bench.py)
   int mode = bwd_mode(D);
-  if (mode == 7 || mode == 8) {
+  if (mode == 7) {
     if (workspace != nullptr && workspace_bytes >= cullavo_attn_bwd_workspace(B, H, Lq, Lk, D, dtype)) {
       u16* ds = (u16*)workspace;
-      const bool pipe = mode == 8;
-#define BDS(DD, CC) bwd_ds_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, ds, s, pipe)
+#define BDS(DD, CC) bwd_ds_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, ds, s)
       if (D == 128) return causal ? BDS(128, true) : BDS(128, false);
       return causal ? BDS(64, true) : BDS(64, false);
 #undef BDS
     }
     mode = 4;  // no dS workspace: the recompute path (same dK / dV kernel)
   }
-  if (mode == 6) {
-#define B64(DD, CC) bwd64_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-    if (D == 128) return causal ? B64(128, true) : B64(128, false);
-    return causal ? B64(64, true) : B64(64, false);
-#undef B64
-  }
-  if (mode == 4 || mode == 5) {
-#define B8(DD, CC, Q8) bwd8_launch<DD, CC, Q8>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
-    if (mode == 5) {
-      if (D == 128) return causal ? B8(128, true, true) : B8(128, false, true);
-      return causal ? B8(64, true, true) : B8(64, false, true);
-    }
-    if (D == 128) return causal ? B8(128, true, false) : B8(128, false, false);
-    return causal ? B8(64, true, false) : B8(64, false, false);
+  if (mode == 4) {
+#define B8(DD, CC) bwd8_launch<DD, CC>(Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv, B, H, Lq, Lk, scale, kv_start, s)
+    if (D == 128) return causal ? B8(128, true) : B8(128, false);
+    return causal ? B8(64, true) : B8(64, false);
 #undef B8
   }
   const int tiles = mode;

@@ -17,8 +17,6 @@
 #include <map>
 #include <mutex>
 
-// the ping-pong kernel (tile modes 12 / 13) lives in gemm_pp.hip (its own translation unit)
-int cvgemm_launch_pp(const cvgemm::GemmArgs& p, int ns, int a_layout, int b_layout, bool f32, hipStream_t s);
 // the decode-step weight-streaming product (M <= 16, forward layouts) lives in gemv.hip
 int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s);
 
@@ -129,7 +127,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_k(GemmArgs p, int splits) {
 // LDS-DMA pieces before its MFMAs, so both waves of a SIMD stall on DMA issue together);
 // 1 = waves 0-3 only, 2 = waves 4-7 only (one loader per SIMD: its DMA issue runs beside the
 // partner wave's MFMAs instead of beside nothing). Data-parallel blocks: one whole tile each,
-// the first sk_dp virtual tiles (all of them without a stream-K tail).
+// the sk_dp tiles of the grid.
 // Fused LoRA up-projection (round 4; the reference recipe's peft adapters, cullavo/load_cullavo.py:
 // 94-112): after the main K loop each lane rounds its base outputs v = round(alpha*acc + bias) into
 // packed bf16 registers, the tile's u rows (this N-tile's module block, 64 wide) and lora_B rows
@@ -256,485 +254,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   }
 }
 
-// Stream-K blocks (launched after the data-parallel ones): block u takes iterations
-// [sk_iters*u/U, sk_iters*(u+1)/U) of the tail tiles (virtual tiles sk_dp.., nk iterations each).
-// A piece that covers a whole tile gets the normal epilogue; a partial piece writes f32 partial
-// sums in fragment order, slot 0 for the block's first piece, 1 for its last (only those two
-// can be partial).
-template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0>
-__global__ __launch_bounds__(512, 1) void gemm256_sk_k(GemmArgs p) {
-  constexpr int BM2 = BMT;
-  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16, TMW = BM2 / 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
-  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
 
-  const int nk = (int)cdiv(p.K, BK);
-  const int unit = xcd_remap(blockIdx.x, p.sk_units);  // neighbouring shares (shared tiles) on one XCD
-  const int64_t base = (int64_t)p.sk_dp * nk;
-  const int64_t it0 = base + p.sk_iters * unit / p.sk_units;
-  const int64_t it1 = base + p.sk_iters * (unit + 1) / p.sk_units;
-  for (int64_t it = it0; it < it1;) {
-    const int kb = (int)(it % nk);
-    const int ke = (int)min((int64_t)nk, kb + (it1 - it));
-    int64_t m0, n0;
-    tile_origin<BM2, BN>(p, (int)(it / nk), m0, n0);
-    f32x4 acc[TMW][TN];
-    tile_k_range<AL, BL, BM2, BN, LDR, TMW, TN>(p, ra, rb, m0, n0, kb, ke, smem, wave, lane, acc);
-    if (kb == 0 && ke == nk) {
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm) {
-        const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4);
-      }
-    } else {
-      float* w = p.sk_ws + ((int64_t)(unit * 2 + (it == it0 ? 0 : 1)) * TMW * TN * 512 + threadIdx.x) * 4;
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          *reinterpret_cast<f32x4*>(w + (int64_t)(tm * TN + tn) * 512 * 4) = acc[tm][tn];
-    }
-    it += ke - kb;
-  }
-}
-
-// Stream-K fix-up: one block per tail tile that more than one block worked on; adds the pieces'
-// f32 partials in K order (fixed, so results are reproducible) and runs the epilogue.
-template <int CT, int BM2, int BN>
-__global__ __launch_bounds__(512) void gemm_sk_fixup_k(GemmArgs p) {
-  constexpr int WN_COLS = BN / 4, TN = WN_COLS / 16, TMW = BM2 / 32;
-  const int64_t nk = cdiv(p.K, BK);
-  const int64_t I = p.sk_iters, U = p.sk_units;
-  const int64_t x0 = (int64_t)blockIdx.x * nk, x1 = x0 + nk - 1;  // the tile's iterations (tail-relative)
-  auto start = [&](int64_t u) { return I * u / U; };
-  auto unit_of = [&](int64_t x) {
-    int64_t u = x * U / I;
-    while (u > 0 && start(u) > x) --u;
-    while (u + 1 < U && start(u + 1) <= x) ++u;
-    return u;
-  };
-  const int64_t u0 = unit_of(x0), u1 = unit_of(x1);
-  if (u0 == u1) return;  // one block ran the whole tile and its epilogue
-  f32x4 acc[TMW][TN];
-#pragma unroll
-  for (int i = 0; i < TMW; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t u = u0; u <= u1; ++u) {
-    if (start(u + 1) == start(u)) continue;  // an empty share
-    const int slot = start(u) >= x0 ? 0 : 1;
-    const float* w = p.sk_ws + ((u * 2 + slot) * TMW * TN * 512 + threadIdx.x) * 4;
-#pragma unroll
-    for (int tm = 0; tm < TMW; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) acc[tm][tn] += *reinterpret_cast<const f32x4*>(w + (int64_t)(tm * TN + tn) * 512 * 4);
-  }
-  int64_t m0, n0;
-  tile_origin<BM2, BN>(p, p.sk_dp + (int)blockIdx.x, m0, n0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 2, wn = wave & 3;
-#pragma unroll
-  for (int tm = 0; tm < TMW; ++tm) {
-    const int64_t m = m0 + wm * (BM2 / 2) + tm * 16 + (lane & 15);
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * WN_COLS + tn * 16 + (lane >> 4) * 4);
-  }
-}
-
-template <int AL, int BL, int CT>
-__global__ __launch_bounds__(512, 1) void gemm4s_k(GemmArgs p) {
-  constexpr int BM2 = 256, BN2 = 256, NST = 4;
-  constexpr int TILE_A = BM2 * BK32 * 2, TILE_B = BN2 * BK32 * 2, STAGE = TILE_A + TILE_B;
-  constexpr int TN = 4, TMW = 8;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * p.tiles_n;
-  const int group = lid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(p.tiles_m - first_m, GROUP_M);
-  const int64_t m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
-  const int64_t n0 = (int64_t)((lid % per_group) / gsize) * BN2;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
-  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
-
-  f32x4 acc[TMW][TN];
-#pragma unroll
-  for (int i = 0; i < TMW; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (int)cdiv(p.K, BK32);
-  auto stage = [&](int t) {
-    char* dst = smem + (t % NST) * STAGE;
-    const int64_t k0 = (int64_t)t * BK32;
-    dma_tile32<AL, BM2>(ra, p.lda, m0, p.M, k0, p.K, dst, wave, lane);
-    dma_tile32<BL, BN2>(rb, p.ldb, n0, p.N, k0, p.K, dst + TILE_A, wave, lane);
-  };
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
-    if (t < nk) stage(t);
-  wait_tiles4(min(NST - 2, nk - 1));  // tile 0 landed
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* cur = smem + (kt % NST) * STAGE;
-    if (kt + NST - 1 < nk) stage(kt + NST - 1);
-    frag8 fb[TN];
-    s16x4 blo[TN], bhi[TN], alo[TMW], ahi[TMW];
-    if constexpr (BL == 1) {
-#pragma unroll
-      for (int t = 0; t < TN; ++t) tr_issue<BN2>(cur + TILE_A, wn * 64 + t * 16, 0, lane, blo[t], bhi[t]);
-    }
-    if constexpr (AL == 1) {
-#pragma unroll
-      for (int tm = 0; tm < TMW; ++tm) tr_issue<BM2>(cur, wm * 128 + tm * 16, 0, lane, alo[tm], ahi[tm]);
-    }
-    if constexpr (BL == 1) tie_all<TN>(blo, bhi);
-    if constexpr (AL == 1) tie_all<TMW>(alo, ahi);
-    if constexpr (AL == 1 || BL == 1) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int t = 0; t < TN; ++t) {
-      if constexpr (BL == 1) {
-        fb[t] = tr_join(blo[t], bhi[t]);
-      } else {
-        const int row = wn * 64 + t * 16 + (lane & 15);
-        fb[t] = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + TILE_A + img0h_off(row, lane >> 4)));
-      }
-    }
-#pragma unroll
-    for (int tm = 0; tm < TMW; ++tm) {
-      frag8 fa;
-      if constexpr (AL == 1) {
-        fa = tr_join(alo[tm], ahi[tm]);
-      } else {
-        const int row = wm * 128 + tm * 16 + (lane & 15);
-        fa = __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(cur + img0h_off(row, lane >> 4)));
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[tn], fa, acc[tm][tn], 0, 0, 0);
-    }
-    // tile kt+1 must have landed before the barrier (tiles up to kt+3 may have been issued)
-    wait_tiles4(min(kt + NST - 1, nk - 1) - (kt + 1));
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
-  if (p.epi_lds) {
-    lds_epilogue<CT, BM2, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
-    return;
-  }
-#pragma unroll
-  for (int tm = 0; tm < TMW; ++tm) {
-    const int64_t m = m0 + wm * 128 + tm * 16 + (lane & 15);
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) store4<CT>(p, acc[tm][tn], m, n0 + wn * 64 + tn * 16 + (lane >> 4) * 4);
-  }
-}
-
-template <int AL, int BL, int CT>
-int launch4s(GemmArgs p, hipStream_t s) {
-  const int smem = 4 * (256 + 256) * BK32 * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm4s_k<AL, BL, CT>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  p.tiles_m = (int)cdiv(p.M, 256);
-  p.tiles_n = (int)cdiv(p.N, 256);
-  gemm4s_k<AL, BL, CT><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
-  return cullavo_check_launch("gemm4s");
-}
-
-// ============================================================================================
-// 256x256 ping-pong kernel: 8 phases per 2 K-tiles, LDS-DMA kept in flight across barriers
-// ============================================================================================
-// LDS (128 KiB): 2 buffers x 4 half-tiles of [128 local rows][64 k] (or [64 k][128]):
-//   A0 = tile rows {0-63, 128-191}   (the m-half 0 rows of wave rows 0 and 1)
-//   A1 = tile rows {64-127, 192-255}
-//   B0 = tile cols {wc*64 + 0..31}, B1 = tile cols {wc*64 + 32..63} for wave cols wc = 0..3
-// Wave (wr, wc) owns output rows wr*128.., cols wc*64..; a K-tile is 4 phases, one C-quadrant
-// (4 m-tiles x 2 n-tiles x K=64 = 16 MFMAs) each:
-//   q0: read B0 sub + A(mh0) sub -> quadrant (mh0, nh0)
-//   q1: read B1 sub               -> (mh0, nh1)
-//   q2: read A(mh1) sub           -> (mh1, nh1)
-//   q3: (no read, B0 kept)        -> (mh1, nh0)
-// so a K-tile's half-tiles are last read at q0 (A0, B0), q1 (B1) and q2 (A1). Every phase stages
-// one half-tile of a later K-tile: q0 -> B1(j+1), q1 -> A1(j+1), q2 -> A0(j+2), q3 -> B0(j+2),
-// each >= 2 phases after the last read of the buffer slot it overwrites (WAR across the two
-// staggered wave groups), and a phase's wait vmcnt(8) (2 DMA instructions per half-tile per
-// wave, 4 half-tiles in flight) retires exactly what the NEXT phase reads (RAW: wait before the
-// phase's first barrier, read one phase later). Waves 4-7 run one barrier behind waves 0-3:
-// each SIMD alternates one wave's LDS reads + DMA issue with the other wave's MFMAs
-// (cdna_hip_programming.md "Pipelining across barriers", §5.5 T3+T4, T5 setprio).
-constexpr int kHalf = 16384;
-
-template <int LAYOUT, int SPL>
-DEV void dma_half(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0,
-                  int64_t K, char* lds, int h, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int pc = wave + 8 * i;  // 16 x 1 KiB pieces per half-tile
-    int lr, k;
-    if (LAYOUT == 0) {
-      lr = pc * 8 + (lane >> 3);
-      k = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
-    } else {
-      const int byte = pc * 1024 + lane * 16;
-      k = byte >> 8;
-      const int b = byte & 255;
-      lr = (((b >> 5) ^ swz1(k)) << 4) + ((b >> 4) & 1) * 8;
-    }
-    const int64_t gi = idx0 + (lr / SPL) * (2 * SPL) + h * SPL + (lr % SPL), gk = k0 + k;
-    unsigned off;
-    if (LAYOUT == 0) off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
-    else off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
-  }
-}
-
-// Loop-invariant part of a half-tile piece's per-lane source offset (K-tile 0, no K-tail
-// check): the K advance goes into the scalar soffset, so the DMA issue in the phase's load
-// segment is two buffer_load ... lds and no per-lane address arithmetic. Out-of-range rows get
-// kOOBv, which stays past num_records with or without the soffset added.
-constexpr unsigned kOOBv = 0x80000000u;
-
-template <int LAYOUT, int SPL>
-DEV unsigned dma_voff(int64_t ld, int64_t idx0, int64_t idx_max, int h, int pc, int lane) {
-  int lr, k;
-  if (LAYOUT == 0) {
-    lr = pc * 8 + (lane >> 3);
-    k = ((lane & 7) ^ ((lr >> 1) & 7)) * 8;
-  } else {
-    const int byte = pc * 1024 + lane * 16;
-    k = byte >> 8;
-    const int b = byte & 255;
-    lr = (((b >> 5) ^ swz1(k)) << 4) + ((b >> 4) & 1) * 8;
-  }
-  const int64_t gi = idx0 + (lr / SPL) * (2 * SPL) + h * SPL + (lr % SPL);
-  if (gi >= idx_max) return kOOBv;
-  return LAYOUT == 0 ? (unsigned)((gi * ld + k) * 2) : (unsigned)(((int64_t)k * ld + gi) * 2);
-}
-
-// 16 x 8 fragment of a half-tile (local rows rbase + lane&15, k = ks*32 + 8*(lane>>4) + j)
-struct HFrag {
-  s16x4 lo, hi;
-};
-
-template <int LAYOUT>
-DEV void hfrag_issue(const char* lds, int rbase, int ks, int lane, HFrag& f) {
-  if (LAYOUT == 0) {
-    const int row = rbase + (lane & 15);
-    const unsigned a = lds_addr(lds + img0_off(row, ks * 4 + (lane >> 4)));
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
-    f.lo = __builtin_shufflevector(v, v, 0, 1, 2, 3);
-    f.hi = __builtin_shufflevector(v, v, 4, 5, 6, 7);
-  } else {
-    tr_issue<128>(lds, rbase, ks, lane, f.lo, f.hi);
-  }
-}
-
-template <int N>
-DEV void hfrag_tie(HFrag (&f)[N]) {
-  static_assert(N == 4 || N == 8, "tie size");
-#pragma unroll
-  for (int i = 0; i < N; i += 4)
-    tr_wait4(f[i].lo, f[i].hi, f[i + 1].lo, f[i + 1].hi, f[i + 2].lo, f[i + 2].hi, f[i + 3].lo, f[i + 3].hi);
-}
-
-DEV frag8 hfrag_val(const HFrag& f) { return tr_join(f.lo, f.hi); }
-
-// wait until at most n (uniform, in half-tiles) of this wave's LDS-DMA half-tiles are in flight
-DEV void wait_halves(int n) {
-  if (n >= 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n == 5) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else if (n == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// S = half-tile slots in LDS (8: 128 KiB, 10: 160 KiB). Half-tiles are issued in the order
-// u = 4j + s (s: 0 A0, 1 B0, 2 B1, 3 A1) into slot u % S, half-tile u during phase u - C
-// (phases 1-indexed, phase 4j+q+1 computes quadrant q of K-tile j), C = S - 3. Then
-//   RAW: the reads of u happen >= C - 1 phases after its issue, H = S - 4 newer half-tiles may
-//        stay in flight at the wait one phase before (vmcnt(2H));
-//   WAR: u + S reuses slot u % S at phase u + S - C = u + 3 >= last read of u (<= u + 1) + 2.
-template <int AL, int BL, int CT, int S>
-__global__ __launch_bounds__(512, 1) void gemm8p_k(GemmArgs p) {
-  static_assert(S == 8 || S == 10, "slot count");
-  constexpr int C = S - 3;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int lid = xcd_remap(blockIdx.x, nwg);
-  constexpr int GROUP_M = 4;
-  const int per_group = GROUP_M * p.tiles_n;
-  const int group = lid / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsize = min(p.tiles_m - first_m, GROUP_M);
-  const int tm_idx = first_m + (lid % per_group) % gsize;
-  const int tn_idx = (lid % per_group) / gsize;
-  const int64_t m0 = (int64_t)tm_idx * 256, n0 = (int64_t)tn_idx * 256;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-
-  const int64_t a_bytes = AL == 0 ? ((p.M - 1) * p.lda + p.K) * 2 : ((p.K - 1) * p.lda + p.M) * 2;
-  const int64_t b_bytes = BL == 0 ? ((p.N - 1) * p.ldb + p.K) * 2 : ((p.K - 1) * p.ldb + p.N) * 2;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, b_bytes);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (int)cdiv(p.K, 64);
-  const int last_u = 4 * nk - 1;
-  auto slot = [&](int u) { return smem + (u % S) * kHalf; };
-  // per-lane source offsets of this wave's 2 pieces of each half-tile kind (A0, A1, B0, B1)
-  unsigned vo[4][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    vo[0][i] = dma_voff<AL, 64>(p.lda, m0, p.M, 0, wave + 8 * i, lane);
-    vo[1][i] = dma_voff<AL, 64>(p.lda, m0, p.M, 1, wave + 8 * i, lane);
-    vo[2][i] = dma_voff<BL, 32>(p.ldb, n0, p.N, 0, wave + 8 * i, lane);
-    vo[3][i] = dma_voff<BL, 32>(p.ldb, n0, p.N, 1, wave + 8 * i, lane);
-  }
-  const bool ktail = (p.K & 63) != 0;
-  auto stage = [&](int u) {
-    const int j = u >> 2, s = u & 3;
-    if (j >= nk) return;
-    char* dst = slot(u);
-    const int64_t k0 = (int64_t)j * 64;
-    const bool isA = s == 0 || s == 3;
-    const int h = isA ? (s == 3) : s - 1;
-    if (ktail && j == nk - 1) {  // zero-fill past K: full per-lane check
-      if (isA) dma_half<AL, 64>(ra, p.lda, m0, p.M, k0, p.K, dst, h, wave, lane);
-      else dma_half<BL, 32>(rb, p.ldb, n0, p.N, k0, p.K, dst, h, wave, lane);
-      return;
-    }
-    const int kind = isA ? h : 2 + h;
-    const int lay = isA ? AL : BL;
-    const int64_t ld = isA ? p.lda : p.ldb;
-    const int soff = (int)(lay == 0 ? k0 * 2 : k0 * ld * 2);
-    const __amdgpu_buffer_rsrc_t r = isA ? ra : rb;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const unsigned v = kind == 0 ? vo[0][i] : kind == 1 ? vo[1][i] : kind == 2 ? vo[2][i] : vo[3][i];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + (wave + 8 * i) * 1024), 16, v, soff, 0, 0);
-    }
-  };
-
-#pragma unroll
-  for (int u = 0; u <= C; ++u) stage(u);
-  wait_halves(min(C, last_u) - 1);  // A0, B0 of K-tile 0 landed
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();
-
-  HFrag fa[8], fb0[4], fb1[4];  // fa: 4 m-tiles x 2 ks of one m-half; fb*: 2 n-tiles x 2 ks
-
-  for (int j = 0; j < nk; ++j) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int mh = q >> 1, nh = (q == 1 || q == 2) ? 1 : 0;
-      const int ub = 4 * j;
-      // DMA first: issued behind a burst of ds_reads an LDS-DMA costs 100-185 cycles of issue
-      // (MI355X_MICROARCH.md cycle constants). Its slot (u_issue % S) is never one this phase
-      // reads (u_issue - u_read is 5..6 for S = 8, 7..8 for S = 10).
-      const int u_issue = ub + q + 1 + C;
-      stage(u_issue);
-      if (q == 0) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) hfrag_issue<BL>(slot(ub + 1), wc * 32 + (t >> 1) * 16, t & 1, lane, fb0[t]);
-      }
-      if (q == 1) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) hfrag_issue<BL>(slot(ub + 2), wc * 32 + (t >> 1) * 16, t & 1, lane, fb1[t]);
-      }
-      if (q == 0 || q == 2) {
-        const char* sa = slot(q == 0 ? ub : ub + 3);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) hfrag_issue<AL>(sa, wr * 64 + (t >> 1) * 16, t & 1, lane, fa[t]);
-      }
-      // the next phase's reads: q0 -> B1(j), q1 -> A1(j), q2 -> none, q3 -> A0/B0(j+1)
-      if (q != 2) {
-        const int need = q == 0 ? ub + 2 : q == 1 ? ub + 3 : ub + 5;
-        if (need <= last_u) wait_halves(min(u_issue, last_u) - need);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      if (q == 0) { hfrag_tie<4>(fb0); hfrag_tie<8>(fa); }
-      if (q == 1) hfrag_tie<4>(fb1);
-      if (q == 2) hfrag_tie<8>(fa);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jn = 0; jn < 2; ++jn) {
-            const HFrag& b = nh ? fb1[jn * 2 + ks] : fb0[jn * 2 + ks];
-            f32x4& c = acc[mh * 4 + i][nh * 2 + jn];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hfrag_val(b), hfrag_val(fa[i * 2 + ks]), c, 0, 0, 0);
-          }
-      }
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();
-
-#pragma unroll
-  for (int tm = 0; tm < 8; ++tm) {
-    const int64_t m = m0 + wr * 128 + tm * 16 + (lane & 15);
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) {
-      const int64_t n = n0 + wc * 64 + tn * 16 + (lane >> 4) * 4;
-      store4<CT>(p, acc[tm][tn], m, n);
-    }
-  }
-}
-
-template <int AL, int BL, int CT, int S>
-int launch8p(GemmArgs p, hipStream_t s) {
-  const int smem = S * kHalf;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_k<AL, BL, CT, S>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  p.tiles_m = (int)cdiv(p.M, 256);
-  p.tiles_n = (int)cdiv(p.N, 256);
-  gemm8p_k<AL, BL, CT, S><<<p.tiles_m * p.tiles_n, 512, smem, s>>>(p);
-  return cullavo_check_launch("gemm8p");
-}
 
 // Split-K plan for the register-staged kernel: products whose 128x128 tile grid cannot fill
 // the 256 CUs but whose K is long (the LoRA adapter GEMMs: N or M = r = 64, K = tokens or
@@ -797,19 +317,6 @@ int launch(const GemmArgs& p, hipStream_t s) {
   return cullavo_check_launch("gemm");
 }
 
-// ---- stream-K tail ---------------------------------------------------------------------------
-// The 8-wave kernels run one block per CU, so a grid of 1376 tiles takes 6 rounds of 256 for
-// 5.375 rounds of work. With a partial last round, the last full round plus the remainder are
-// given to 256 blocks as equal shares of their K-iterations (each block: whole tiles where its
-// share covers them, f32 partial sums for the at most two tiles it shares), and a fix-up
-// kernel adds each shared tile's partials in K order and runs the epilogue. Auto mode uses it
-// when the last round would leave at least g_sk_min_idle of the CUs idle: the partial sums'
-// round trip through HBM has to be paid for. Off by default: measured on the 7B step's shapes
-// (tools/streamk_bench.py, profiles/r02/streamk_bench.log) it loses 5-43 % -- the partials'
-// write + fix-up read (~0.6 of a round at K = 4096) eat the recovered tail, and the stream-K
-// kernel's piece loop pushes the dW variant past 256 VGPRs (spills).
-int g_streamk = 0;             // 0 off, 1 auto, 2 whenever the last round is partial
-double g_sk_min_idle = 0.25;
 
 int num_cus() {
   static int n = 0;
@@ -821,98 +328,30 @@ int num_cus() {
   return n;
 }
 
-// one scratch buffer per (device, stream), allocated once at the largest size any 8-wave
-// launch can ask for (2 partial tiles of 256x256 f32 per CU); launches on one stream are
-// ordered, so they can share it
-float* sk_workspace(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, void*> pool;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> g(mu);
-  auto it = pool.find({dev, s});
-  if (it != pool.end()) return (float*)it->second;
-  void* ptr = nullptr;
-  if (hipMalloc(&ptr, (size_t)num_cus() * 2 * 256 * 256 * 4) != hipSuccess) ptr = nullptr;
-  pool[{dev, s}] = ptr;
-  return (float*)ptr;
-}
 
-template <int AL, int BL, int CT, int BM2, int BN2, int LDR = 0, bool LORA = false>
+template <int AL, int BL, int CT, int BM2, int BN2, bool LORA = false>
 int launch256(GemmArgs p, hipStream_t s) {
-  // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB);
-  // then the prefetch's 256-B dummy slot
-  p.pf_lds = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
-  const int smem = p.pf_lds + 256;
+  // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB)
+  const int smem = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA>,
+    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
   p.tiles_m = (int)cdiv(p.M, BM2);
   p.tiles_n = (int)cdiv(p.N, BN2);
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n, nk = cdiv(p.K, BK);
+  p.sk_dp = (int)tiles;
   if (p.part) {  // split-K over the 8-wave kernel (small grids, splitk256_plan), then the reduce
     const int splits = (int)cdiv(nk, p.kt_per);
-    p.sk_dp = (int)tiles;
-    p.sk_units = 0;
-    gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
+    gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
     const int64_t work = p.M * (p.N / 4);
     splitk_reduce_k<CT><<<(int)std::min<int64_t>(cdiv(work, 256), 4096), 256, 0, s>>>(p, splits);
     return cullavo_check_launch("gemm256 split-K");
   }
-  const int slots = num_cus();
-  const int64_t full = tiles / slots, rem = tiles % slots;
-  p.sk_dp = (int)tiles;
-  p.sk_units = 0;
-  p.sk_iters = 0;
-  p.sk_ws = nullptr;
-  const bool want = g_streamk != 0 && rem != 0 && nk >= 4 &&
-                    (g_streamk == 2 || (double)(slots - rem) / slots >= g_sk_min_idle);
-  if (want) {
-    float* ws = sk_workspace(s);
-    if (ws != nullptr) {
-      const int64_t dp = full >= 1 ? (full - 1) * slots : 0;
-      p.sk_dp = (int)dp;
-      p.sk_iters = (tiles - dp) * nk;
-      p.sk_units = (int)std::min<int64_t>(slots, p.sk_iters);
-      p.sk_ws = ws;
-    }
-  }
-  if (p.sk_dp > 0) gemm256_k<AL, BL, CT, BM2, BN2, LDR, LORA><<<p.sk_dp, 512, smem, s>>>(p);
-  if (p.sk_units > 0) {
-    static bool sk_attr = false;
-    if (!sk_attr) {
-      (void)hipFuncSetAttribute((const void*)gemm256_sk_k<AL, BL, CT, BM2, BN2, LDR>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-      sk_attr = true;
-    }
-    gemm256_sk_k<AL, BL, CT, BM2, BN2, LDR><<<p.sk_units, 512, smem, s>>>(p);
-    gemm_sk_fixup_k<CT, BM2, BN2><<<(unsigned)(tiles - p.sk_dp), 512, 0, s>>>(p);
-  }
+  gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA><<<(unsigned)tiles, 512, smem, s>>>(p);
   return cullavo_check_launch("gemm256");
-}
-
-// Which waves stage the next K-tile (tools/gemm_bench.py, same-run A/B on the model's shapes):
-// one loader wave per SIMD. With a K-contiguous A it won 7-14 % in round 1; for the transposed
-// weight-gradient products all eight waves loading won 10-15 % then, but with the precomputed DMA
-// offsets (round 3) one loader per SIMD is 5-11 % faster there too (tile 6 vs 2 on the five 7B
-// dW shapes, profiles/r03/ldr/gemm_bench.txt).
-template <int AL, int BL>
-constexpr int default_ldr() { return 1; }
-
-// tile modes 6 / 7: the 256x256 / 192x256 kernels with the other loader choice (A/B testing)
-template <int AL, int BL>
-int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
-  constexpr int L = 1 - default_ldr<AL, BL>();
-  if constexpr (AL == 0) {
-    if (tile == 7)
-      return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256, L>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256, L>(p, s);
-    if (tile == 11)  // 288 rows, all eight waves loading (36 A pieces: 5 or 4 per wave)
-      return f32 ? launch256<0, BL, CULLAVO_DT_F32, 288, 256, L>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 288, 256, L>(p, s);
-  }
-  return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256, L>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256, L>(p, s);
 }
 
 // Kernel-shape choice. Time model = FLOPs / (per-tile rate of the shape) x (whole rounds of
@@ -921,19 +360,19 @@ int launch_alt_ldr(GemmArgs p, int tile, bool f32, hipStream_t s) {
 // measured on MI355X with tools/gemm_bench.py): 256x256 ~1300, 192x256
 // ~1150 (A K-contiguous only; the 256-row tile reads 14 % less LDS per MFMA), 128x128 4-wave
 // (2 blocks/CU, 512 slots) ~840.
-// kT8p / kT8p10 (the ping-pong kernel) are selectable but not auto-chosen: measured against
-// the 2-stage kernels on the model's shapes (tools/gemm_bench.py, several boxes) they win
-// 3-7 % on big-N forward products (q|k|v, lm_head), lose 10-25 % on dX, dW and N = 4096,
-// and the box-to-box spread (~10 %) is larger than their forward gain. With the steady DMA
-// removed the same schedule reaches hipBLASLt's rate (gate|up 1483 vs 1382 TF/s), so the
-// remaining loss is LDS-DMA issue cost inside the load segment (profiles/r01/gemm_8phase.md).
+// Measured slower and moved out of the library in round 5 (sources in tools/lab/ and git history,
+// records under profiles/): the 8-phase / ping-pong kernels (round-1 modes 4/5 and round-4 modes
+// 12/13/15/16: +3-7 % on big-N forward products, -10-25 % on dX, dW and N = 4096;
+// profiles/r01/gemm_8phase.md, profiles/r04/gemm/), the BK=32 4-stage kernel (mode 8, slower on every
+// step shape, profiles/r02/gemm_lab.md), the stream-K tail (-5-43 %, profiles/r02/streamk_bench.log),
+// the all-waves-loading alternatives (modes 6/7/11, profiles/r03/ldr/), the L2 prefetch of K-tile
+// kt+2 (-5-12 %, profiles/r03/prefetch/) and the 256x128 tile (mode 1, never chosen).
 // kT288x256 (round 3): 288-row tiles for a K-contiguous A (9 MFMA rows per wave, 36 A pieces
 // over the 4 loader waves). The per-K-tile overhead (barrier, DMA issue, fragment-read latency)
 // is roughly fixed, so a taller tile amortises it over more MFMAs, and M = 8704 = 30.2 x 288
 // makes the N = 4096 products (every dX, o and down forward) 496 tiles = 1.94 rounds instead of
 // 736 192-row tiles = 2.88 rounds.
-enum { kT128 = 0, kT256x128 = 1, kT256x256 = 2, kT192x256 = 3, kT8p = 4, kT8p10 = 5, kT4s = 8, kT288x256 = 10,
-       kTpp4 = 12, kTpp5 = 13, kTpp4x32 = 15, kTpp5x32 = 16 };
+enum { kT128 = 0, kT256x256 = 2, kT192x256 = 3, kT288x256 = 10 };
 // plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
 double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
@@ -965,19 +404,13 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
 }  // namespace
 
 static int g_force_tile = -1;
-static int g_gemv = 1;  // cullavo_gemm_set_tile(0..13) forces a tiled kernel for decode rows too
+static int g_gemv = 1;  // cullavo_gemm_set_tile(mode >= 0) forces a tiled kernel for decode rows too
 static bool gemv_eligible(int64_t M, int a_layout, int b_layout, bool dropping) {
   return g_gemv && g_force_tile < 0 && M >= 1 && M <= 16 && a_layout == 0 && b_layout == 0 && !dropping;
 }
 static int g_epi_lds = 1;
 static int g_nt_store = 0;
 static int g_dma_pre = 1;  // +2.7 % on the 7B step (profiles/r03/dma_ab.md)
-// L2 prefetch of K-tile kt+2 in the 8-wave loop (cullavo_gemm_set_prefetch): measured slower on
-// every 7B shape (5-12 %) and on the step (376.9 / 377.4 vs 351.1 / 350.6 ms alternating,
-// profiles/r03/prefetch/): the loop is bound by LDS-DMA issue, not by the data's arrival, so one
-// more memory instruction per wave and K-step costs more than the L2 hits save. Off.
-static int g_prefetch = 0;
-static int g_loaders_all = 0;  // cullavo_gemm_set_loaders: 1 = all eight waves load on layout-1 A (dW)
 // Groups of 4 N-tiles sweeping the M-tiles: measured against groups of 4 M-tiles on every 7B
 // step shape in one process (profiles/r02/closing/group_sweep.txt), 1-5 % faster on 13 of 15.
 static int g_group_m = -4;
@@ -994,17 +427,9 @@ extern "C" int cullavo_gemm_set_group(int group) {
   return prev;
 }
 
-extern "C" int cullavo_gemm_set_streamk(int mode) {
-  const int prev = g_streamk;
-  if (mode >= 0 && mode <= 2) g_streamk = mode;
-  return prev;
-}
-
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = ((mode >= 0 && mode <= 8) || mode == kT288x256 || mode == 11 || mode == kTpp4 || mode == kTpp5 ||
-                   mode == kTpp4x32 || mode == kTpp5x32) ? mode
-                                                                                                        : -1;
+  g_force_tile = (mode == kT128 || mode == kT256x256 || mode == kT192x256 || mode == kT288x256) ? mode : -1;
   return prev;
 }
 
@@ -1015,18 +440,6 @@ extern "C" int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previou
   if (previous) *previous = (float)g_tile_rate[i];
   g_tile_rate[i] = tflops > 0.f ? (double)tflops : 0.0;
   return CULLAVO_OK;
-}
-
-extern "C" int cullavo_gemm_set_loaders(int mode) {
-  const int prev = g_loaders_all;
-  g_loaders_all = mode & 1;
-  return prev;
-}
-
-extern "C" int cullavo_gemm_set_prefetch(int on) {
-  const int prev = g_prefetch;
-  g_prefetch = on & 1;
-  return prev;
 }
 
 // A/B switch for the precomputed-offset LDS-DMA loop of the 8-wave 256-row kernels
@@ -1059,10 +472,9 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
   }
   int tile = choose_tile(M, N, K, a_layout, g_force_tile);
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
-  if ((tile == 7 || tile == 11) && a_layout != 0) tile = 6;
-  static const int bm[17] = {128, 256, 256, 192, 256, 256, 256, 192, 256, 256, 288, 288, 256, 256, 16, 256, 256};
-  static const int bn[17] = {128, 128, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 16, 256, 256};
-  if (grid) *grid = cdiv(M, bm[tile]) * cdiv(N, bn[tile]);
+  const int bm = tile == kT128 ? 128 : tile == kT192x256 ? 192 : tile == kT288x256 ? 288 : 256;
+  const int bn = tile == kT128 ? 128 : 256;
+  if (grid) *grid = cdiv(M, bm) * cdiv(N, bn);
   (void)b_layout;
   return tile;
 }
@@ -1117,9 +529,6 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   p.part = nullptr;
   p.kt_per = 0;
   p.sk_dp = 0;
-  p.sk_units = 0;
-  p.sk_iters = 0;
-  p.sk_ws = nullptr;
   p.group_m = g_group_m;
   {
     auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
@@ -1128,8 +537,6 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   }
   p.nt_store = g_nt_store;
   p.dma_pre = g_dma_pre && (a_layout == 1 || K % BK == 0) && (b_layout == 1 || K % BK == 0);
-  p.pf = g_prefetch;
-  p.pf_lds = 0;
   p.lora_u = nullptr;
   p.lora_b = nullptr;
   p.ld_lu = 0;
@@ -1154,8 +561,8 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     p.lora_scale = d.lora_scale;
     // the 288-row tile where the plan takes it (the N = 4096 products: 2 rounds instead of 3)
     if (choose_tile(M, N, K, 0, g_force_tile) == kT288x256)
-      return launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1, true>(p, s);
-    return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, default_ldr<0, 0>(), true>(p, s);
+      return launch256<0, 0, CULLAVO_DT_BF16, 288, 256, true>(p, s);
+    return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, true>(p, s);
   }
   // decode rows (M = batch <= 16, Y = X W^T): stream W once through the GEMV kernel (gemv.hip)
   if (gemv_eligible(M, a_layout, b_layout, dropping)) return cvgemm_launch_gemv(p, f32, s);
@@ -1181,44 +588,19 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
     if (a_layout == 0) return f32 ? launch<0, 1, CULLAVO_DT_F32, 2>(p, s) : launch<0, 1, CULLAVO_DT_BF16, 2>(p, s);
     return f32 ? launch<1, 1, CULLAVO_DT_F32, 2>(p, s) : launch<1, 1, CULLAVO_DT_BF16, 2>(p, s);
   }
-  if (tile == kT8p || tile == kT8p10) {
-#define L8P(AL, BL)                                                                                          \
-  if (tile == kT8p) return f32 ? launch8p<AL, BL, CULLAVO_DT_F32, 8>(p, s) : launch8p<AL, BL, CULLAVO_DT_BF16, 8>(p, s); \
-  return f32 ? launch8p<AL, BL, CULLAVO_DT_F32, 10>(p, s) : launch8p<AL, BL, CULLAVO_DT_BF16, 10>(p, s);
-    if (a_layout == 0 && b_layout == 0) { L8P(0, 0) }
-    if (a_layout == 0 && b_layout == 1) { L8P(0, 1) }
-    if (a_layout == 1 && b_layout == 0) { L8P(1, 0) }
-    L8P(1, 1)
-#undef L8P
-  }
-  if (tile == kTpp4 || tile == kTpp5 || tile == kTpp4x32 || tile == kTpp5x32)
-    return cvgemm_launch_pp(p, tile == kTpp4 ? 4 : tile == kTpp5 ? 5 : tile == kTpp4x32 ? 14 : 15, a_layout, b_layout,
-                            f32, s);
-  if (tile == kT4s) {
-#define L4S(AL, BL) return f32 ? launch4s<AL, BL, CULLAVO_DT_F32>(p, s) : launch4s<AL, BL, CULLAVO_DT_BF16>(p, s);
-    if (a_layout == 0 && b_layout == 0) { L4S(0, 0) }
-    if (a_layout == 0 && b_layout == 1) { L4S(0, 1) }
-    if (a_layout == 1 && b_layout == 0) { L4S(1, 0) }
-    L4S(1, 1)
-#undef L4S
-  }
   if (tile == kT288x256) {  // a_layout 0 (above), one loader wave per SIMD
     if (b_layout == 0)
-      return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
-    return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256, 1>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256, 1>(p, s);
+      return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256>(p, s);
+    return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256>(p, s);
   }
-  if (g_loaders_all && a_layout == 1 && tile == kT256x256) tile = 6;  // A/B: the round-2 dW loader choice
-  if (tile >= 6) {
-    if (a_layout == 0 && b_layout == 0) return launch_alt_ldr<0, 0>(p, tile, f32, s);
-    if (a_layout == 0 && b_layout == 1) return launch_alt_ldr<0, 1>(p, tile, f32, s);
-    if (a_layout == 1 && b_layout == 0) return launch_alt_ldr<1, 0>(p, tile, f32, s);
-    return launch_alt_ldr<1, 1>(p, tile, f32, s);
+  if (tile == kT192x256) {
+    if (b_layout == 0)
+      return f32 ? launch256<0, 0, CULLAVO_DT_F32, 192, 256>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 192, 256>(p, s);
+    return f32 ? launch256<0, 1, CULLAVO_DT_F32, 192, 256>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 192, 256>(p, s);
   }
-  if (tile != kT128) {
-#define L256(AL, BL)                                                                                       \
-  if (tile == kT256x256) return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256, default_ldr<AL, BL>()>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256, default_ldr<AL, BL>()>(p, s); \
-  if (tile == kT192x256 && AL == 0) return f32 ? launch256<0, BL, CULLAVO_DT_F32, 192, 256, default_ldr<0, BL>()>(p, s) : launch256<0, BL, CULLAVO_DT_BF16, 192, 256, default_ldr<0, BL>()>(p, s); \
-  return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 128>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 128>(p, s);
+  if (tile == kT256x256) {
+#define L256(AL, BL) \
+  return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256>(p, s);
     if (a_layout == 0 && b_layout == 0) { L256(0, 0) }
     if (a_layout == 0 && b_layout == 1) { L256(0, 1) }
     if (a_layout == 1 && b_layout == 0) { L256(1, 0) }

@@ -34,16 +34,10 @@ struct GemmArgs {
   int kt_per;         // K-tiles per split
   int epi_lds;        // 8-wave kernels: LDS-staged 16-B epilogue (all pointers 16-B aligned)
   int nt_store;       // C written with non-temporal stores (streamed past the caches)
-  // stream-K tail of the 8-wave kernels (sk_units = 0: off): blocks < sk_dp run whole tiles;
-  // the sk_units blocks after them split the sk_iters K-iterations of the remaining tiles evenly
-  int sk_dp, sk_units;
-  int64_t sk_iters;
-  float* sk_ws;       // f32 partials [sk_units][2][512 threads x TMW*TN f32x4], fragment order
+  int sk_dp;          // 8-wave kernels: tiles in the grid (the XCD remap's block count)
   int group_m;        // 8-wave tile order: > 0 groups of group_m M-tiles sweep N; < 0 groups of
                       // -group_m N-tiles sweep M
   int dma_pre;        // 8-wave 256-row kernels: per-lane DMA offsets precomputed, K advance in soffset
-  int pf;             // 8-wave 256-row kernels: L2 prefetch of K-tile kt+2 (with dma_pre only)
-  int pf_lds;         // byte offset of the prefetch's dummy LDS slot (past stages and epilogue image)
   // fused LoRA up-projection (gemm256_k<..., LORA = true>): t = round(lora_scale * u_m B_m^T) for
   // the module m = n / lora_out of each output column, added to round(alpha*acc + bias)
   const u16* lora_u;  // [M, n_mod * 64] (row stride ld_lu): lora_A outputs of the group's modules
@@ -515,31 +509,6 @@ DEV void dma_issue(__amdgpu_buffer_rsrc_t rsrc, const unsigned* vo, int soff, ch
   }
 }
 
-// L2 prefetch of K-tile kt + 2 (round 3). The 2-stage loop gives each K-tile's LDS-DMA one
-// tile of MFMAs (~2,000 cycles) to land, and the dW / forward panels mostly miss the 4 MB L2
-// (PMC: ~4x the algorithmic bytes come from the Infinity Cache / HBM), so misses sit in the
-// per-tile vmcnt(0). One extra 4-byte-per-lane LDS-DMA per wave touches every 128-B line of
-// the tile two K-steps ahead (A lines on waves 0-3, B lines on waves 4-7; a line per lane),
-// pulling it into L2 a tile early; its data lands in a dummy LDS slot nobody reads, so it
-// needs no register and no ordering, only a counted wait (vmcnt(1) instead of 0: it is the
-// wave's youngest memory operation). Out-of-range rows get kOOBp (dropped by the range check).
-// Lines of a layout-0 operand: one per row (64 k = 128 B); of a layout-1 operand: ROWS*2/128
-// per k-row.
-template <int LAYOUT, int ROWS>
-DEV unsigned pf_prep(int64_t ld, int64_t idx0, int64_t idx_max, int li) {
-  int64_t gi, rel;
-  if (LAYOUT == 0) {
-    gi = idx0 + li;
-    rel = gi * ld;
-  } else {
-    constexpr int LPR = ROWS * 2 / 128;  // lines per k-row
-    const int k = li / LPR, ch = li % LPR;
-    gi = idx0 + ch * 64;
-    rel = (int64_t)k * ld + gi;
-  }
-  return gi < idx_max ? (unsigned)(rel * 2) : kOOBp;
-}
-
 // scalar byte offset of K-tile origin k0 for an operand of layout L
 template <int L>
 DEV int dma_soff(int64_t k0, int64_t ld) { return (int)(L == 0 ? k0 * 2 : k0 * ld * 2); }
@@ -687,11 +656,6 @@ DEV int tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buff
     unsigned va[dma_per<BM2, NWL>()], vb[dma_per<BN, NWL>()];
     dma_prep<AL, BM2, NWL>(p.lda, m0, p.M, lw, lane, va);
     dma_prep<BL, BN, NWL>(p.ldb, n0, p.N, lw, lane, vb);
-    // prefetch lanes: waves 0-3 the first 256 A lines, waves 4-7 the B lines
-    const bool pf_a = wave < 4;
-    const unsigned vpf = pf_a ? pf_prep<AL, BM2>(p.lda, m0, p.M, wave * 64 + lane)
-                              : pf_prep<BL, BN>(p.ldb, n0, p.N, (wave - 4) * 64 + lane);
-    char* pf_slot = smem + p.pf_lds;
     for (int kt = kb; kt < ke; ++kt) {
       char* cur = smem + ((kt - kb) & 1) * STAGE;
       char* nxt = smem + ((kt - kb + 1) & 1) * STAGE;
@@ -703,17 +667,9 @@ DEV int tile_k_range(const GemmArgs& p, __amdgpu_buffer_rsrc_t ra, __amdgpu_buff
       if constexpr (LPF) {
         if (kt + 1 == ke) lora_stage<BM2, BN>(p, m0, n0, nxt, wave, lane);
       }
-      const bool pf = p.pf && kt + 2 < ke;  // uniform
-      if (pf) {
-        const int64_t k2 = (int64_t)(kt + 2) * BK;
-        if (pf_a) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)pf_slot, 4, vpf, dma_soff<AL>(k2, p.lda), 0, 0);
-        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)pf_slot, 4, vpf, dma_soff<BL>(k2, p.ldb), 0, 0);
-      }
       tile_mfma<AL, BL, BM2, BN, TMW, TN>(cur, wm, wn, lane, acc);
-      // every DMA of tile kt+1 landed; the prefetch (this wave's youngest operation) may fly on.
-      // A raw s_barrier: __syncthreads()'s fence would add vmcnt(0) and wait for the prefetch.
-      if (pf) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every DMA of tile kt+1 landed (raw s_barrier: the compiler emits no extra wait)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -771,59 +727,5 @@ DEV void tile_origin(const GemmArgs& p, int lid, int64_t& m0, int64_t& n0) {
   m0 = (int64_t)(first_m + (lid % per_group) % gsize) * BM2;
   n0 = (int64_t)((lid % per_group) / gsize) * BN;
 }
-
-// ============================================================================================
-// 256x256 tile, BK = 32, 4 LDS stages: LDS-DMA kept two K-tiles ahead across raw barriers
-// ============================================================================================
-// The 2-stage kernel above drains vmcnt(0) + a full barrier every K-tile, so each tile's DMA
-// has one tile of MFMAs (~1,000 cycles per SIMD) to land: L2 misses are exposed
-// (cdna_hip_programming.md "Pipelining across barriers": 3-buffer span beats 2-buffer overlap
-// at ~1 block/CU). Here a stage is a 32-deep K-tile (A 16 KiB + B 16 KiB), four stages fill
-// 128 KiB, tile kt+3 is issued while tile kt is computed, and the wait before each raw
-// s_barrier only retires tile kt+1 (vmcnt(8): tiles kt+2, kt+3 stay in flight).
-//   RAW: tile kt+1 is waited for before the barrier that ends iteration kt and read after it.
-//   WAR: slot (kt+3)%4 held tile kt-1, whose fragments were all read (and consumed by MFMAs)
-//        before the barrier that ended iteration kt-1, which precedes this issue.
-// Layout-0 images are [rows][32 k] with 64-B rows: 16-B chunk c of row r sits at slot
-// c ^ ((r >> 2) & 2), which makes every ds_read_b128 lane group of 16 hit 16 distinct bank slots
-// (rows r..r+15 of one fragment, chunks 0/1 or 2/3 per group). Layout-1 images are [32 k][rows]
-// read with ds_read_b64_tr_b16, as in the 64-deep kernels.
-constexpr int BK32 = 32;
-
-DEV int img0h_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 2)) << 4); }
-
-// one [ROWS][32] (layout 0) or [32][ROWS] (layout 1) operand image, 8 waves
-template <int LAYOUT, int ROWS>
-DEV void dma_tile32(__amdgpu_buffer_rsrc_t rsrc, int64_t ld, int64_t idx0, int64_t idx_max, int64_t k0, int64_t K,
-                    char* lds, int wave, int lane) {
-  constexpr int kPieces = ROWS / 16;  // 1 KiB pieces: 16 rows of 64 B, or 2 k-rows of ROWS*2 B (ROWS = 256)
-#pragma unroll
-  for (int i = 0; i < kPieces / 8; ++i) {
-    const int pc = wave + 8 * i;
-    unsigned off;
-    if (LAYOUT == 0) {
-      const int row = pc * 16 + (lane >> 2);
-      const int chunk = (lane & 3) ^ ((row >> 2) & 2);
-      const int64_t gi = idx0 + row, gk = k0 + chunk * 8;
-      off = (gi < idx_max && gk < K) ? (unsigned)((gi * ld + gk) * 2) : kOOB;
-    } else {
-      constexpr int RB = ROWS * 2;
-      const int byte = pc * 1024 + lane * 16;
-      const int k = byte / RB, b = byte % RB;
-      const int unit = (b >> 5) ^ swz1(k), half = (b >> 4) & 1;
-      const int64_t gk = k0 + k, gi = idx0 + unit * 16 + half * 8;
-      off = (gk < K && gi < idx_max) ? (unsigned)((gk * ld + gi) * 2) : kOOB;
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + pc * 1024), 16, off, 0, 0, 0);
-  }
-}
-
-// retire all but n (wave-uniform, in K-tiles of 4 DMA instructions) of this wave's tiles
-DEV void wait_tiles4(int n) {
-  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 
 }  // namespace cvgemm

@@ -49,9 +49,11 @@ extern "C" {
 #define CULLAVO_ACT_SWIGLU_BWD 3
 
 /* ABI version: bumped whenever an exported signature changes (2: cullavo_im2col_patches gained
-   out_dtype, cullavo_vision_embed_ln dtype, cullavo_gemm_desc f32_operands). A consumer built
-   against this header checks cullavo_abi_version() == CULLAVO_ABI_VERSION at load. */
-#define CULLAVO_ABI_VERSION 3
+   out_dtype, cullavo_vision_embed_ln dtype, cullavo_gemm_desc f32_operands; 4: the tuning switches
+   of the measured-slower GEMM variants removed with them: cullavo_gemm_set_streamk,
+   cullavo_gemm_set_prefetch, cullavo_gemm_set_loaders). A consumer built against this header
+   checks cullavo_abi_version() == CULLAVO_ABI_VERSION at load. */
+#define CULLAVO_ABI_VERSION 4
 
 int cullavo_abi_version(void);
 const char* cullavo_last_error(void);
@@ -138,17 +140,10 @@ size_t cullavo_gemm_desc_size(void);
 size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
 
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
- * 4 waves, 1 = 256x128 / 8 waves, 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves (LDS-DMA
- * staged; 3 falls back to 2 when A is not K-contiguous), 4 / 5 = 256x256 ping-pong kernel
- * with 8 / 10 LDS half-tile slots (128 / 160 KiB, DMA kept in flight across barriers),
- * 6 / 7 = modes 2 / 3 with the other loader-wave choice (A/B testing), 8 = 256x256 with
- * 32-deep K-tiles in 4 LDS stages (DMA two K-tiles ahead across raw barriers), 10 = 288x256 /
- * 8 waves (falls back to 2 when A is not K-contiguous; chosen automatically only for K >= 2048),
- * 11 = mode 10 with the other loader-wave choice (A/B testing), 12 / 13 = the 256x256
- * ping-pong wave-group kernel (two 4-wave groups alternating MFMA and LDS-DMA phases; 4 / 5
- * LDS stages, 16x16x32 MFMAs), 15 / 16 = modes 12 / 13 with 32x32x16 MFMAs (all four measured
- * slower than modes 2 / 10 on the 7B step shapes, profiles/r04/gemm/; never chosen
- * automatically; need a_layout = b_layout = 0).
+ * 4 waves (register staged), 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves, 10 = 288x256 / 8 waves
+ * (LDS-DMA staged; 3 and 10 fall back to 2 when A is not K-contiguous; 10 is chosen automatically
+ * only for K >= 2048). Other values select automatic. The measured-slower variants of earlier
+ * rounds (ping-pong / 8-phase, BK = 32 4-stage, 256x128, other loader waves) were removed in ABI 4.
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
 /* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
@@ -156,13 +151,6 @@ int cullavo_gemm_set_tile(int mode);
    shape from the automatic choice (0 on mode 10 = round-2 behaviour). *previous (nullable)
    receives the old rate. Tuning/A-B switch; not thread-safe. */
 int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous);
-/* Stream-K tail of the 8-wave kernels: 0 = off (default; slower on every 7B step shape
-   measured), 1 = auto (when a partial last round of tiles would leave >= 25 % of the CUs
-   idle), 2 = whenever the last round is partial. The
-   tail's f32 partial sums go to a library-owned scratch buffer, one per (device, stream)
-   (2 x 256x256 f32 per CU, allocated at first use); a fix-up kernel adds them in K order.
-   Returns the previous mode. For tests and tuning; not thread-safe. */
-int cullavo_gemm_set_streamk(int mode);
 /* Tile order of the 8-wave kernels (tuning/A-B switch): > 0 = groups of that many M-tiles
    sweep the N-tiles, < 0 = groups of -group N-tiles sweep the M-tiles (default -4); each XCD
    walks a contiguous run of the order. 0 leaves the setting. Returns the previous setting. */
@@ -180,17 +168,6 @@ int cullavo_gemm_set_epilogue(int lds_staged);
    or the operand is stored [K][rows], layout 1; the default); 0 = offsets recomputed per
    K-tile. Same results either way. Returns the previous setting. */
 int cullavo_gemm_set_dma(int precomputed);
-/* Tuning/A-B switch for the 8-wave 256-row kernels (with the precomputed-offset loop): 1 =
-   every K-step also touches the 128-B lines of the tile two K-steps ahead (one 4-byte-per-lane
-   LDS-DMA per wave into a dummy LDS slot), so they are L2-resident when their real LDS-DMA is
-   issued; 0 (default: measured 5-12 % slower with it on) = off. Same results either way.
-   Returns the previous setting. */
-int cullavo_gemm_set_prefetch(int on);
-/* Tuning/A-B switch for the 8-wave kernels' LDS-DMA loader waves on products with a layout-1 A
-   (the weight gradients): 0 (default) = one loader wave per SIMD, as for every other product;
-   1 = all eight waves load (the round-2 choice, 5-11 % slower with the precomputed offsets).
-   Same results either way. Returns the previous setting. */
-int cullavo_gemm_set_loaders(int mode);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
  * 9 = the 8-wave 256x256 kernel split over K (a grid of at most half the CUs with >= 32
@@ -298,17 +275,14 @@ int cullavo_attn_bwd_ws(const void* q, int64_t ldq, const void* k, int64_t ldk, 
 size_t cullavo_attn_bwd_workspace(int B, int H, int Lq, int Lk, int D, int dtype);
 /* Tuning/A-B switch for cullavo_attn_bwd: 4 = the 8-wave dK/dV kernel (two waves per SIMD;
    waves w and w+4 split each query tile and add their partial sums once, in a fixed order)
-   with the 4-wave 32-key dQ kernel; 5 = both kernels 8-wave; 0-3 = the 4-wave kernels;
-   6 = 64 keys per wave dK/dV (4 waves, one per SIMD; bitwise equal to 0-3); 7 = mode 4's dK/dV
-   kernel storing dS^T + dQ from it (needs the cullavo_attn_bwd_ws workspace); 8 = mode 7's
-   products with the software-pipelined dK/dV kernel (one wave per SIMD, K / V in registers,
-   a 3-slot Q / dO ring; the same dS^T values, dK / dV summed in sweep order: bitwise equal to
-   mode 1) and the streaming dQ-from-dS kernel (3-slot ring, two tiles in flight);
-   -1 (the default) = 7 for D=128 (4 through cullavo_attn_bwd, which has no workspace), 2 for
+   with the 4-wave 32-key dQ kernel; 0-3 = the 4-wave kernels; 7 = mode 4's dK/dV
+   kernel storing dS^T + dQ from it (needs the cullavo_attn_bwd_ws workspace); -1 (the default) = 7 for D=128 (4 through cullavo_attn_bwd, which has no workspace), 2 for
    D=64 (measured per head dim).
    In 0-3 with bit 0 = 64 query rows per dK/dV barrier, bit 1 = 64
    keys per dQ barrier (else 32) -- results bitwise identical across 0-3 (same products summed
-   in the same order). Out-of-range values leave the mode unchanged. Returns the previous mode. */
+   in the same order). Modes 5, 6 and 8 (measured slower: both kernels 8-wave, 64 keys per wave,
+   the software-pipelined mode-7 pair; profiles/r02/attn/, profiles/r04/attn/) were removed in
+   round 5. Other values leave the mode unchanged. Returns the previous mode. */
 int cullavo_attn_set_bwd_tiles(int mode);
 /* A/B switch for the attention forward's K/V tile staging: 2 = 16-B buffer loads
    through a per-tile scalar descriptor (one loop-invariant lane offset, rows past the sequence

@@ -41,7 +41,7 @@ def close(out, ref, tol, what):
     assert err <= tol * scale, f"{what}: max|err| {err:.3e} > {tol:.1e} * {scale:.3e}"
 
 
-@pytest.mark.parametrize("tile", [-1, 2, 6])
+@pytest.mark.parametrize("tile", [-1, 2, 10])
 @pytest.mark.parametrize("al,bl", [(1, 1), (1, 0), (0, 1), (0, 0)])
 @pytest.mark.parametrize("K", [1000, 1160, 4096])
 def test_gemm_k_tail_reads_zeros_next_to_nan(tile, al, bl, K):
@@ -133,7 +133,7 @@ def test_attention_rows_past_end_next_to_nan(B, H, L, D, causal):
     prev_s = Lb.cullavo_attn_set_bwd_stage(0)
     try:
         base = None
-        for tiles in ((7, 4, 8) if D == 128 else (0, 4, 8)):
+        for tiles in ((7, 4) if D == 128 else (0, 4)):
             Lb.cullavo_attn_set_bwd_tiles(tiles)
             for st in (0, 1, 2, 3):
                 Lb.cullavo_attn_set_bwd_stage(st)
