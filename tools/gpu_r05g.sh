@@ -1,0 +1,7 @@
+#!/bin/bash
+# ablations of the 4-wave GEMM (tools/lab/gemm4w_lab.hip)
+set -o pipefail
+OUT=gpurun_out/r05g
+mkdir -p $OUT
+timeout -k 10 300 python -u tools/lab/gemm_lab.py --lib tools/lab/bin/libgemm4w_lab.so --variants 0,128,1000 --shapes gate_up,lm_head --prod > $OUT/abl.txt 2>&1; rc=$?
+cat $OUT/abl.txt; exit $rc

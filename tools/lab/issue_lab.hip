@@ -3,7 +3,9 @@
 // loop question behind it: is an LDS-DMA piece (buffer_load_dwordx4 ... lds) dearer to issue
 // beside MFMAs than the register-staging pair (buffer_load_dwordx4 -> VGPR, ds_write_b128)?
 //
-// Per iteration each wave issues 8 independent MFMAs (random bf16 operands in registers) and
+// Per iteration each wave issues 8 MFMAs on 8 independent accumulators (random bf16 operands in
+// registers; round 5, second version: the first alternated two accumulators, whose dependent
+// chains left bubbles the memory instructions hid in) and
 //   V0: nothing else
 //   V1: one LDS-DMA piece (1 KiB per wave-instruction, L2-resident source)
 //   V2: one buffer_load_dwordx4 into VGPRs (its value consumed 4 loads later)
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(512) void issue_k(const unsigned char* __restrict__
   u32x4 r0 = {0, 0, 0, 0}, r1 = r0, r2 = r0, r3 = r0, sink = r0;
   char* lds_w = smem + wave * 8192;
   const unsigned lds_a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds_w + lane * 16;
-  f32x4 c0 = acc[0], c1 = acc[1];
+  f32x4 c0 = acc[0], c1 = acc[1], c2 = acc[2], c3 = acc[3], c4 = acc[4], c5 = acc[5], c6 = acc[6], c7 = acc[7];
   // every instruction of the loop is inline asm (volatile: issued in program order, nothing hoisted
   // or merged); the register loads' values are consumed 4 iterations later behind a counted vmcnt(3)
 #define MF(c) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(fa), "v"(fb) : "memory")
@@ -86,18 +88,17 @@ __global__ __launch_bounds__(512) void issue_k(const unsigned char* __restrict__
         u32x4 x, y;
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:4096" : "=v"(x), "=v"(y) : "v"(lds_a + u * 1024)
                      : "memory");
-        MF(c1); MF(c0); MF(c1);
+        MF(c1); MF(c2); MF(c3);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x), "+v"(y) :: "memory");
         sink ^= x ^ y;
-        MF(c0); MF(c1); MF(c0); MF(c1);
+        MF(c4); MF(c5); MF(c6); MF(c7);
         continue;
       }
-      MF(c1); MF(c0); MF(c1); MF(c0); MF(c1); MF(c0); MF(c1);
+      MF(c1); MF(c2); MF(c3); MF(c4); MF(c5); MF(c6); MF(c7);
     }
   }
 #undef MF
-  acc[0] = c0;
-  acc[1] = c1;
+  acc[0] = c0; acc[1] = c1; acc[2] = c2; acc[3] = c3; acc[4] = c4; acc[5] = c5; acc[6] = c6; acc[7] = c7;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float s = 0.f;
 #pragma unroll
