@@ -19,9 +19,6 @@
 
 // the decode-step weight-streaming product (M <= 16, forward layouts) lives in gemv.hip
 int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s);
-// the 4-wave 256x256 kernel (tile mode 4) lives in gemm4w.hip
-bool cvgemm_4w_eligible(const cvgemm::GemmArgs& p, int a_layout, int b_layout);
-int cvgemm_launch_4w(const cvgemm::GemmArgs& p, int a_layout, int b_layout, bool f32, hipStream_t s);
 
 namespace {
 using namespace cvgemm;
@@ -375,17 +372,17 @@ int launch256(GemmArgs p, hipStream_t s) {
 // is roughly fixed, so a taller tile amortises it over more MFMAs, and M = 8704 = 30.2 x 288
 // makes the N = 4096 products (every dX, o and down forward) 496 tiles = 1.94 rounds instead of
 // 736 192-row tiles = 2.88 rounds.
-// kT4w (round 5, gemm4w.hip): 256x256 with four waves, AGPR accumulators and a register-staged
-// pipeline two K-tiles deep; in the automatic choice once its plan rate is set above 0.
-enum { kT128 = 0, kT256x256 = 2, kT192x256 = 3, kT4w = 4, kT288x256 = 10 };
-// plan rates of tile modes 2, 3, 10, 4 (cullavo_gemm_set_tile_rate)
-double g_tile_rate[4] = {1300.0, 1150.0, 1360.0, 0.0};
+// Round 5 tried a 4-wave 256x256 kernel (one wave per SIMD, AGPR accumulators, register- or
+// LDS-DMA-staged, with and without a stream-K head): equal or slower on every step shape, kept
+// in tools/lab/gemm4w_r5.hip with its ablations (profiles/r05/gemm/).
+enum { kT128 = 0, kT256x256 = 2, kT192x256 = 3, kT288x256 = 10 };
+// plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
+double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
-  const C cands[5] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, g_tile_rate[0]},
-                      {kT192x256, 192, 256, 256, g_tile_rate[1]}, {kT288x256, 288, 256, 256, g_tile_rate[2]},
-                      {kT4w, 256, 256, 256, g_tile_rate[3]}};
+  const C cands[4] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, g_tile_rate[0]},
+                      {kT192x256, 192, 256, 256, g_tile_rate[1]}, {kT288x256, 288, 256, 256, g_tile_rate[2]}};
   double best = 1e300;
   int bid = kT128;
   for (const C& c : cands) {
@@ -435,14 +432,13 @@ extern "C" int cullavo_gemm_set_group(int group) {
 
 extern "C" int cullavo_gemm_set_tile(int mode) {
   const int prev = g_force_tile;
-  g_force_tile = (mode == kT128 || mode == kT256x256 || mode == kT192x256 || mode == kT288x256 || mode == kT4w) ? mode
-                                                                                                              : -1;
+  g_force_tile = (mode == kT128 || mode == kT256x256 || mode == kT192x256 || mode == kT288x256) ? mode : -1;
   return prev;
 }
 
 extern "C" int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous) {
-  const int i = mode == kT256x256 ? 0 : mode == kT192x256 ? 1 : mode == kT288x256 ? 2 : mode == kT4w ? 3 : -1;
-  CV_REQUIRE(i >= 0, CULLAVO_EINVAL, "tile rate: mode must be 2, 3, 4 or 10");
+  const int i = mode == kT256x256 ? 0 : mode == kT192x256 ? 1 : mode == kT288x256 ? 2 : -1;
+  CV_REQUIRE(i >= 0, CULLAVO_EINVAL, "tile rate: mode must be 2, 3 or 10");
   CV_REQUIRE(i != 0 || tflops > 0.f, CULLAVO_EINVAL, "tile rate: mode 2 cannot be removed");
   if (previous) *previous = (float)g_tile_rate[i];
   g_tile_rate[i] = tflops > 0.f ? (double)tflops : 0.0;
@@ -594,10 +590,6 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   if (p.drop_mode == 2) {
     if (a_layout == 0) return f32 ? launch<0, 1, CULLAVO_DT_F32, 2>(p, s) : launch<0, 1, CULLAVO_DT_BF16, 2>(p, s);
     return f32 ? launch<1, 1, CULLAVO_DT_F32, 2>(p, s) : launch<1, 1, CULLAVO_DT_BF16, 2>(p, s);
-  }
-  if (tile == kT4w) {
-    if (cvgemm_4w_eligible(p, a_layout, b_layout)) return cvgemm_launch_4w(p, a_layout, b_layout, f32, s);
-    tile = kT256x256;  // K tail on a K-contiguous operand or an unaligned epilogue: the 8-wave kernel
   }
   if (tile == kT288x256) {  // a_layout 0 (above), one loader wave per SIMD
     if (b_layout == 0)

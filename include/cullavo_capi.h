@@ -142,13 +142,12 @@ size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
  * 4 waves (register staged), 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves, 10 = 288x256 / 8 waves
  * (LDS-DMA staged; 3 and 10 fall back to 2 when A is not K-contiguous; 10 is chosen automatically
- * only for K >= 2048), 4 = 256x256 / 4 waves (accumulators in AGPRs, register-staged pipeline two
- * K-tiles deep; falls back to 2 for a K tail on a K-contiguous operand or an unaligned epilogue;
- * in the automatic choice only with a plan rate > 0, cullavo_gemm_set_tile_rate). Other values select automatic. The measured-slower variants of earlier
- * rounds (ping-pong / 8-phase, BK = 32 4-stage, 256x128, other loader waves) were removed in ABI 4.
+ * only for K >= 2048). Other values select automatic. The measured-slower variants of earlier
+ * rounds (ping-pong / 8-phase, BK = 32 4-stage, 256x128, other loader waves, the round-5 4-wave
+ * 256x256 kernel) are not in the library (ABI 4; tools/lab).
  * Returns the previous mode. For tests and tuning; not thread-safe. */
 int cullavo_gemm_set_tile(int mode);
-/* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3, 4 or 10
+/* Per-tile rate (TFLOP/s) the automatic kernel-shape choice assumes for tile mode 2, 3 or 10
    (its time model: FLOPs / rate x whole rounds of tiles over the CUs); rate <= 0 removes the
    shape from the automatic choice (0 on mode 10 = round-2 behaviour). *previous (nullable)
    receives the old rate. Tuning/A-B switch; not thread-safe. */

@@ -3,5 +3,5 @@
 set -o pipefail
 OUT=gpurun_out/r05g
 mkdir -p $OUT
-timeout -k 10 300 python -u tools/lab/gemm_lab.py --lib tools/lab/bin/libgemm4w_lab.so --variants 0,128,1000 --shapes gate_up,lm_head --prod > $OUT/abl.txt 2>&1; rc=$?
+timeout -k 10 300 python -u tools/lab/gemm_lab.py --lib tools/lab/bin/libgemm4w_lab.so --variants 2001,2000,2001,2000 --shapes gate_up,lm_head,qkv,o,down --prod > $OUT/abl.txt 2>&1; rc=$?
 cat $OUT/abl.txt; exit $rc
