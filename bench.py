@@ -504,6 +504,8 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, 1, false>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false> split-K + splitk_reduce_k<1>",
              10: f"gemm256_k<{al}, {bl}, 1, 288, 256, 1, {lf}>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
+    if tile >= 100:  # the M-tail split: the head rows' kernel (+ a thin split-K product for the rest)
+        return names.get(tile - 100, f"tile{tile - 100}<{al}, {bl}>") + " M-split", int(g.value)
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 

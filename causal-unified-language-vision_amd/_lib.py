@@ -97,6 +97,8 @@ def lib():
             L.cullavo_gemm_set_tile(int(os.environ["CULLAVO_GEMM_TILE"]))
         if os.environ.get("CULLAVO_SPLITK_TARGET"):  # split-K plan A/B (cullavo_gemm_set_splitk_target)
             L.cullavo_gemm_set_splitk_target(int(os.environ["CULLAVO_SPLITK_TARGET"]))
+        if os.environ.get("CULLAVO_GEMM_MSPLIT"):  # M-tail split A/B (cullavo_gemm_set_msplit)
+            L.cullavo_gemm_set_msplit(int(os.environ["CULLAVO_GEMM_MSPLIT"]))
         if os.environ.get("CULLAVO_GEMM_GROUP"):  # tile-order A/B (cullavo_gemm_set_group)
             L.cullavo_gemm_set_group(int(os.environ["CULLAVO_GEMM_GROUP"]))
         if os.environ.get("CULLAVO_GEMM_DMA"):  # DMA-offset A/B (cullavo_gemm_set_dma)

@@ -378,13 +378,29 @@ int launch256(GemmArgs p, hipStream_t s) {
 enum { kT128 = 0, kT256x256 = 2, kT192x256 = 3, kT288x256 = 10 };
 // plan rates of tile modes 2, 3, 10 (cullavo_gemm_set_tile_rate)
 double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
-int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
+// M-tail split (round 5): when M is just past a multiple of a tile's height, its last M-tile row
+// is mostly padding and can cost a whole extra round (the ViT's M = 64 x 577 = 36928 = 144 x 256
+// + 64: fc1 at 256x256 is 2,320 tiles = 9.06 rounds -> 10; fc2 / o at 288x256 are 516 tiles =
+// 2.02 rounds -> 3). The plan then runs rows [0, m_main) (m_main = a multiple of the tile height)
+// on that tile and the remaining rows as a second, thin product (128x128 tiles, split over K
+// when the caller gives the workspace), if that is estimated at least 5 % faster.
+int g_msplit = 1;
+double rem_seconds(int64_t rows, int64_t N, int64_t K) { return 2.0 * rows * N * K / 200e12 + 6e-6; }
+
+int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_t* m_main = nullptr) {
+  if (m_main) *m_main = 0;
   if (force >= 0) return force;
   struct C { int id; int64_t bm, bn, slots; double rate; };
   const C cands[4] = {{kT128, 128, 128, 512, 840.0}, {kT256x256, 256, 256, 256, g_tile_rate[0]},
                       {kT192x256, 192, 256, 256, g_tile_rate[1]}, {kT288x256, 288, 256, 256, g_tile_rate[2]}};
-  double best = 1e300;
-  int bid = kT128;
+  // time = whole rounds of tiles x one round (a tile's FLOPs over the per-CU share of the rate)
+  auto seconds = [&](const C& c, int64_t m) {
+    const int64_t tiles = cdiv(m, c.bm) * cdiv(N, c.bn);
+    return (double)cdiv(tiles, c.slots) * 2.0 * c.bm * c.bn * K * c.slots / (c.rate * 1e12);
+  };
+  double best = 1e300, best_split = 1e300;
+  int bid = kT128, bid_split = kT128;
+  int64_t mm_split = 0;
   for (const C& c : cands) {
     if ((c.id == kT192x256 || c.id == kT288x256) && a_layout != 0) continue;
     // 288 rows only for long K: with 16 K-tiles (the ViT's K = 1024 products) its larger
@@ -392,15 +408,18 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force) {
     // fc1 36928x4096x1024 at 815 TF/s against 865 for the 256-row tile)
     if (c.id == kT288x256 && K < 2048) continue;
     if (c.rate <= 0.0) continue;
-    const int64_t tiles = cdiv(M, c.bm) * cdiv(N, c.bn);
-    const double exact = (double)tiles / (double)c.slots;
-    const double rounds = (double)cdiv(tiles, c.slots);
-    // padded work of partial edge tiles is paid too
-    const double eff_area = (double)(M * N) / (double)(tiles * c.bm * c.bn);
-    const double t = (rounds / exact) / (c.rate * eff_area);
+    const double t = seconds(c, M);
     if (t < best * 0.999) { best = t; bid = c.id; }
+    const int64_t mm = M / c.bm * c.bm;
+    if (m_main && g_msplit && c.id != kT128 && mm > 0 && mm < M) {
+      const double ts = seconds(c, mm) + rem_seconds(M - mm, N, K);
+      if (ts < best_split * 0.999) { best_split = ts; bid_split = c.id; mm_split = mm; }
+    }
   }
-  (void)K;
+  if (m_main && best_split < 0.95 * best) {
+    *m_main = mm_split;
+    return bid_split;
+  }
   return bid;
 }
 
@@ -473,16 +492,45 @@ extern "C" int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, 
       return 9;
     }
   }
-  int tile = choose_tile(M, N, K, a_layout, g_force_tile);
+  int64_t mm = 0;
+  int tile = choose_tile(M, N, K, a_layout, g_force_tile, &mm);
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
-  const int bm = tile == kT128 ? 128 : tile == kT192x256 ? 192 : tile == kT288x256 ? 288 : 256;  // 2, 4: 256
+  const int bm = tile == kT128 ? 128 : tile == kT192x256 ? 192 : tile == kT288x256 ? 288 : 256;  // 2: 256
   const int bn = tile == kT128 ? 128 : 256;
-  if (grid) *grid = cdiv(M, bm) * cdiv(N, bn);
+  if (grid) *grid = cdiv(mm > 0 ? mm : M, bm) * cdiv(N, bn);
   (void)b_layout;
-  return tile;
+  return mm > 0 ? 100 + tile : tile;
 }
 
-static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
+static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint = -1);
+
+// rows [m0, M) of the product d as a product of its own (every row-indexed operand shifted)
+static cullavo_gemm_desc rows_from(const cullavo_gemm_desc& d, int64_t m0) {
+  cullavo_gemm_desc r = d;
+  const int64_t cz = d.c_dtype == CULLAVO_DT_F32 ? 4 : 2;
+  r.M = d.M - m0;
+  r.A = (const char*)d.A + (d.a_layout == 0 ? m0 * d.lda : m0) * 2;
+  r.C = (char*)d.C + m0 * d.ldc * cz;
+  if (d.preact) r.preact = (char*)d.preact + m0 * d.ldc * 2;
+  if (d.residual) r.residual = (const char*)d.residual + m0 * d.ldr * 2;
+  if (d.addend) r.addend = (const char*)d.addend + m0 * d.ld_addend * 2;
+  if (d.lora_u) r.lora_u = (const char*)d.lora_u + m0 * d.ld_lora_u * 2;
+  return r;
+}
+
+// the M-tail split of d (rows of the head product; its tile in *tile), or 0 (choose_tile)
+static int64_t msplit_rows(const cullavo_gemm_desc& d, int* tile = nullptr) {
+  if (d.f32_operands || (d.drop_operand != 0 && d.drop_p > 0.f) || d.M <= 16 || d.N <= 0 || d.K <= 0) return 0;
+  const int64_t a_ext = d.a_layout == 0 ? (d.M - 1) * d.lda + d.K : (d.K - 1) * d.lda + d.M;
+  const int64_t b_ext = d.b_layout == 0 ? (d.N - 1) * d.ldb + d.K : (d.K - 1) * d.ldb + d.N;
+  if (a_ext * 2 >= (int64_t)kOOB || b_ext * 2 >= (int64_t)kOOB) return 0;  // the kT128 path
+  int64_t mm = 0;
+  const int t = choose_tile(d.M, d.N, d.K, d.a_layout, g_force_tile, &mm);
+  if (tile) *tile = t;
+  return mm;
+}
+
+static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
   const int a_layout = d.a_layout, b_layout = d.b_layout, c_dtype = d.c_dtype, act = d.act;
   const int64_t M = d.M, N = d.N, K = d.K, lda = d.lda, ldb = d.ldb, ldc = d.ldc, ldr = d.ldr;
   const void* residual = d.residual;
@@ -515,6 +563,19 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
   CV_REQUIRE(d.lora_u == nullptr || !d.f32_operands, CULLAVO_EUNSUPPORTED, "fused LoRA: bf16 operands only");
   if (d.f32_operands) return cullavo_gemm_f32_impl(d, CV_STREAM(stream));  // gemm_f32.hip
   if (M == 0 || N == 0) return CULLAVO_OK;
+  if (tile_hint < 0 && !gemv_eligible(M, a_layout, b_layout, d.drop_operand != 0 && d.drop_p > 0.f)) {
+    int head_tile = 0;
+    const int64_t mm = msplit_rows(d, &head_tile);
+    if (mm > 0) {  // whole rounds on the planned tile, then the remaining rows (see choose_tile)
+      cullavo_gemm_desc head = d;
+      head.M = mm;
+      head.workspace = nullptr;
+      head.workspace_bytes = 0;
+      const int rc = gemm_impl(head, stream, head_tile);
+      if (rc != CULLAVO_OK) return rc;
+      return gemm_impl(rows_from(d, mm), stream, -1);
+    }
+  }
   const int64_t tm = cdiv(M, BM), tn = cdiv(N, BN);
   CV_REQUIRE(tm * tn < (1ll << 31), CULLAVO_EINVAL, "too many tiles");
   GemmArgs p;
@@ -581,7 +642,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream) {
       split256 = s256 > 1;
     }
   }
-  int tile = dma_ok ? choose_tile(M, N, K, a_layout, g_force_tile) : kT128;
+  int tile = dma_ok ? (tile_hint >= 0 ? tile_hint : choose_tile(M, N, K, a_layout, g_force_tile)) : kT128;
   // 288-row layout-1 A images do not fit the register budget of the transposed-read kernel
   // (197 VGPRs spilled): the weight-gradient products keep the 256-row tile
   if ((tile == kT192x256 || tile == kT288x256) && a_layout != 0) tile = kT256x256;
@@ -632,6 +693,11 @@ extern "C" size_t cullavo_gemm_desc_size(void) { return sizeof(cullavo_gemm_desc
 
 extern "C" size_t cullavo_gemm_workspace(const cullavo_gemm_desc* d) {
   if (d == nullptr || d->M <= 0 || d->N <= 0 || d->K <= 0 || g_force_tile >= 0) return 0;
+  const int64_t mm = msplit_rows(*d);
+  if (mm > 0) {  // only the remaining rows' product can be split over K
+    const cullavo_gemm_desc r = rows_from(*d, mm);
+    return cullavo_gemm_workspace(&r);
+  }
   const bool dma_layouts = d->drop_operand != 1 && d->drop_operand != 2;
   const int s256 = dma_layouts ? splitk256_plan(d->M, d->N, d->K, nullptr) : 1;
   const int splits = s256 > 1 ? s256 : splitk_plan(d->M, d->N, d->K, nullptr);
@@ -641,4 +707,11 @@ extern "C" size_t cullavo_gemm_workspace(const cullavo_gemm_desc* d) {
 extern "C" int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream) {
   CV_REQUIRE(desc != nullptr, CULLAVO_EINVAL, "desc");
   return gemm_impl(*desc, stream);
+}
+
+// A/B switch for the M-tail split of the automatic plan (1 = on, the default); returns the previous
+extern "C" int cullavo_gemm_set_msplit(int on) {
+  const int prev = g_msplit;
+  g_msplit = on ? 1 : 0;
+  return prev;
 }

@@ -94,11 +94,13 @@ def trace_launches():
 
 
 def _split256(M, N, K, a_layout, b_layout) -> bool:
-    """the library runs this problem split over K on the 8-wave kernel (cullavo_gemm_plan tile 9:
-    a small 256x256 grid with a long K), given a workspace from the caller. Asked per call, not
-    cached: the plan depends on the library's forced tile and tile rates (cullavo_gemm_set_tile /
-    _set_tile_rate), which callers may change at any time (one ~1 us host call per GEMM)."""
-    return lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None) == 9
+    """the library splits this problem over K given a workspace from the caller: cullavo_gemm_plan
+    tile 9 (a small 256x256 grid with a long K on the 8-wave kernel) or 100 + t (the M-tail split,
+    whose thin second product runs split-K). Asked per call, not cached: the plan depends on the
+    library's forced tile and tile rates (cullavo_gemm_set_tile / _set_tile_rate), which callers
+    may change at any time (one ~1 us host call per GEMM)."""
+    t = lib().cullavo_gemm_plan(M, N, K, a_layout, b_layout, None)
+    return t == 9 or t >= 100
 
 
 def gemm(a_layout: int, b_layout: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, *,

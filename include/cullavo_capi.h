@@ -152,6 +152,11 @@ int cullavo_gemm_set_tile(int mode);
    shape from the automatic choice (0 on mode 10 = round-2 behaviour). *previous (nullable)
    receives the old rate. Tuning/A-B switch; not thread-safe. */
 int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous);
+/* M-tail split of the automatic plan (tuning/A-B switch, 1 = on, the default): when M is just past
+   a multiple of the chosen tile height, the head rows run on that tile in whole rounds and the
+   remaining rows as a second, thin product (split over K when cullavo_gemm_workspace sized the
+   caller's workspace for it). Returns the previous setting. */
+int cullavo_gemm_set_msplit(int on);
 /* Tile order of the 8-wave kernels (tuning/A-B switch): > 0 = groups of that many M-tiles
    sweep the N-tiles, < 0 = groups of -group N-tiles sweep the M-tiles (default -4); each XCD
    walks a contiguous run of the order. 0 leaves the setting. Returns the previous setting. */
@@ -176,7 +181,11 @@ int cullavo_gemm_set_dma(int precomputed);
  * cullavo_gemm_workspace() asks for; f32 partials [splits][M][N], reduced in split order
  * (deterministic) with the full epilogue. cullavo_gemm itself (no workspace) never splits.
  * 14 = the weight-streaming decode product (gemv.hip: M <= 16 rows, a_layout = b_layout = 0,
- * automatic tile mode, no dropout): one 8-wave workgroup per 16 rows of B, no workspace. */
+ * automatic tile mode, no dropout): one 8-wave workgroup per 16 rows of B, no workspace.
+ * 100 + t = the M-tail split (cullavo_gemm_set_msplit): the first rows in whole rounds of tile
+ * mode t (*grid = that launch's workgroups), the remaining rows as a second product, split over
+ * K only when the caller passes the workspace cullavo_gemm_workspace() asks for (cullavo_gemm_ex;
+ * cullavo_gemm runs them unsplit). */
 int cullavo_gemm_plan(int64_t M, int64_t N, int64_t K, int a_layout, int b_layout, int64_t* grid);
 
 /* ---- norms -------------------------------------------------------------------------------

@@ -93,6 +93,39 @@ def test_gemm_epilogues(act, tile_mode, epi_mode):
     close(y, a.to(BF).float() + r.float(), 8e-3, "epilogue")
 
 
+@pytest.mark.parametrize("M,N,K,act", [(36928, 1024, 4096, "none"), (36928, 4096, 1024, "quick_gelu"),
+                                         (36928, 1024, 1024, "none")])
+def test_gemm_msplit(M, N, K, act):
+    """M-tail split (cullavo_gemm_set_msplit; the ViT's M = 64 x 577 = 36928): the head rows run in
+    whole rounds of the planned tile and the rest as a thin split-K product. Head rows are
+    bit-identical to the same tile run over all of M (cullavo_gemm_set_tile), the tail rows match
+    the fp32 product (bias, quick_gelu and residual in the epilogue of both parts)."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    plan = L.cullavo_gemm_plan(M, N, K, 0, 0, None)
+    assert plan >= 100, plan
+    tile = plan - 100
+    bm = {2: 256, 3: 192, 10: 288}[tile]
+    mm = M // bm * bm
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(M, K, device=DEV, generator=g).to(BF)
+    w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(BF)
+    b = (torch.randn(N, device=DEV, generator=g) * 0.1).to(BF)
+    r = torch.randn(M, N, device=DEV, generator=g).to(BF)
+    code = ops().ACT_QUICK_GELU if act == "quick_gelu" else ops().ACT_NONE
+    y = ops().linear(x, w, b, act=code, residual=r)
+    prev = L.cullavo_gemm_set_tile(tile)
+    try:
+        y_tile = ops().linear(x, w, b, act=code, residual=r)
+    finally:
+        L.cullavo_gemm_set_tile(prev)
+    assert torch.equal(y[:mm], y_tile[:mm])
+    p = (x[mm:].float() @ w.float().T + b.float()).to(BF).float()
+    a = O.quick_gelu(p) if act == "quick_gelu" else p
+    close(y[mm:], a.to(BF).float() + r[mm:].float(), 8e-3, "tail rows")
+    close(y[:mm][::97], y_tile[:mm][::97], 0.0, "head rows")
+
+
 @pytest.mark.parametrize("act", ["gelu", "quick_gelu"])
 def test_gemm_epilogue_paths_bit_identical(tile_mode, act):
     """The LDS-staged 16-B epilogue (packed quick_gelu) and the per-lane one compute the same
