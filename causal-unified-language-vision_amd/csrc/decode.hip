@@ -33,28 +33,82 @@ __global__ __launch_bounds__(256) void kv_append_k(const u16* __restrict__ ks, i
   }
 }
 
-template <int D>
+// ROPE (cullavo_attn_decode_rope): the step's RoPE + KV append fused in front (rope_append8_k's
+// arithmetic, elementwise.hip): every workgroup rotates its head's query row itself (q is read, not
+// rotated in place), the workgroup whose chunk holds the new row start[b] rotates that row's key,
+// writes key and value to the cache and uses them from LDS (its own loads of that row may predate
+// the write), and the keys attended are [kv_start[b], start[b] + 1).
+struct DecodeRope {
+  const u16* k;
+  int64_t ldk;
+  const u16* v;
+  int64_t ldv;
+  const int64_t* pos;
+  float theta;
+  const int32_t* start;
+  u16* kc;
+  u16* vc;
+};
+
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, int64_t ldq, const u16* __restrict__ Kc,
                                                     const u16* __restrict__ Vc, int64_t ld_tok, int64_t ld_b,
                                                     const int32_t* __restrict__ kv_len,
                                                     const int32_t* __restrict__ kv_start, float scale_log2,
                                                     float* __restrict__ part_o, float* __restrict__ part_ml,
-                                                    int H, int nchunk) {
+                                                    int H, int nchunk, DecodeRope rp = DecodeRope{}) {
   static_assert(D == 128, "decode attention is specialised for the LM head_dim");
   const int c = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int t = threadIdx.x;
-  const int len = kv_len[b], k_lo = kv_start ? kv_start[b] : 0;
+  const int pnew = ROPE ? rp.start[b] : -1;  // the appended row (ROPE)
+  const int len = ROPE ? pnew + 1 : kv_len[b], k_lo = kv_start ? kv_start[b] : 0;
   const int kbeg = c * kChunk, kend = min(len, kbeg + kChunk);
   __shared__ float qs[D];
   __shared__ float ps[kChunk];
   __shared__ float red[8];
   __shared__ float oacc[16][D];
+  __shared__ float cs[D / 2], sn[D / 2];
+  __shared__ u16 kn[D], vn[D];
   const int64_t pidx = ((int64_t)b * H + h) * nchunk + c;
   if (kbeg >= kend) {  // chunk past this row's length: empty partial
     if (t < D) part_o[pidx * D + t] = 0.f;
     if (t == 0) { part_ml[2 * pidx] = -INFINITY; part_ml[2 * pidx + 1] = 0.f; }
   } else {
-    if (t < D) qs[t] = bf2f(Q[(int64_t)b * ldq + (int64_t)h * D + t]) * scale_log2;
+    const bool has_new = ROPE && pnew >= kbeg && pnew < kend;
+    if constexpr (ROPE) {
+      if (t < D / 2) {
+        const float inv_freq = 1.0f / powf(rp.theta, (float)(2 * t) / (float)D);
+        const float ang = (float)rp.pos[b] * inv_freq;
+        cs[t] = Elt<u16>::rnd(cosf(ang));
+        sn[t] = Elt<u16>::rnd(sinf(ang));
+      }
+      __syncthreads();
+      // t < 64: the query pair (t, t + 64); 64 <= t < 128 (the new row's chunk): the key pair
+      if (t < D / 2 || (has_new && t < D)) {
+        const int i = t & (D / 2 - 1);
+        const u16* src = t < D / 2 ? Q + (int64_t)b * ldq + (int64_t)h * D : rp.k + (int64_t)b * rp.ldk + (int64_t)h * D;
+        const float x1 = bf2f(src[i]), x2 = bf2f(src[i + D / 2]);
+        const float o1 = Elt<u16>::rnd(Elt<u16>::rnd(x1 * cs[i]) + Elt<u16>::rnd(-x2 * sn[i]));
+        const float o2 = Elt<u16>::rnd(Elt<u16>::rnd(x2 * cs[i]) + Elt<u16>::rnd(x1 * sn[i]));
+        if (t < D / 2) {
+          qs[i] = o1 * scale_log2;
+          qs[i + D / 2] = o2 * scale_log2;
+        } else {
+          const int64_t row = (int64_t)b * ld_b + (int64_t)pnew * ld_tok + (int64_t)h * D;
+          kn[i] = f2bf(o1);
+          kn[i + D / 2] = f2bf(o2);
+          rp.kc[row + i] = f2bf(o1);
+          rp.kc[row + i + D / 2] = f2bf(o2);
+        }
+      }
+      if (has_new && t >= D && t < 2 * D) {
+        const u16 vv = rp.v[(int64_t)b * rp.ldv + (int64_t)h * D + (t - D)];
+        vn[t - D] = vv;
+        rp.vc[(int64_t)b * ld_b + (int64_t)pnew * ld_tok + (int64_t)h * D + (t - D)] = vv;
+      }
+    } else {
+      if (t < D) qs[t] = bf2f(Q[(int64_t)b * ldq + (int64_t)h * D + t]) * scale_log2;
+    }
     const u16* Kb = Kc + (int64_t)b * ld_b + (int64_t)h * D;
     const u16* Vb = Vc + (int64_t)b * ld_b + (int64_t)h * D;
     // scores: 8 lanes per key (16 dims each, one 256 B row per key), 32 keys per pass; the K rows
@@ -80,6 +134,25 @@ __global__ __launch_bounds__(256) void attn_decode_k(const u16* __restrict__ Q, 
       vr[i] = *reinterpret_cast<const u16x8*>(Vb + (int64_t)(kbeg + k) * ld_tok + dg * 8);
     }
     __syncthreads();
+    if (has_new) {  // the appended row from LDS (this workgroup's own cache write may not be visible)
+#pragma unroll
+      for (int pass = 0; pass < kPass; ++pass) {
+        if (min(kbeg + pass * 32 + slot, kend - 1) == pnew) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            kr[pass][0][j] = kn[sub * 16 + j];
+            kr[pass][1][j] = kn[sub * 16 + 8 + j];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kChunk / 16; ++i) {
+        if (kbeg + min(kg + 16 * i, nk - 1) == pnew) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vr[i][j] = vn[dg * 8 + j];
+        }
+      }
+    }
     float qv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) qv[j] = qs[sub * 16 + j];
@@ -195,6 +268,30 @@ extern "C" int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int6
 extern "C" size_t cullavo_attn_decode_workspace(int B, int H, int max_len, int D) {
   const int64_t nchunk = cdiv((int64_t)std::max(max_len, 1), kChunk);
   return (size_t)B * H * nchunk * (D + 2) * sizeof(float);
+}
+
+extern "C" int cullavo_attn_decode_rope(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                                        int64_t ldv, const int64_t* position_ids, float theta, void* k_cache,
+                                        void* v_cache, int64_t ld_tok, int64_t ld_batch, const int32_t* start,
+                                        const int32_t* kv_start, void* o, int64_t ldo, int B, int H, int max_len,
+                                        int D, float scale, float* workspace, void* stream) {
+  CV_REQUIRE(D == 128, CULLAVO_EUNSUPPORTED, "decode attention: head_dim 128");
+  CV_REQUIRE(start != nullptr && position_ids != nullptr && workspace != nullptr && k != nullptr && v != nullptr,
+             CULLAVO_EINVAL, "decode attention + rope: start / position_ids / workspace / k / v");
+  CV_REQUIRE(ld_tok >= (int64_t)H * D && ldq >= (int64_t)H * D && ldk >= (int64_t)H * D && ldv >= (int64_t)H * D &&
+                 ldo >= (int64_t)H * D && ld_tok % 8 == 0,
+             CULLAVO_EINVAL, "decode attention + rope: strides");
+  if (B == 0 || H == 0 || max_len <= 0) return CULLAVO_OK;
+  hipStream_t s = CV_STREAM(stream);
+  const int nchunk = (int)cdiv((int64_t)max_len, kChunk);
+  float* part_o = workspace;
+  float* part_ml = workspace + (int64_t)B * H * nchunk * D;
+  DecodeRope rp{(const u16*)k, ldk, (const u16*)v, ldv, position_ids, theta, start, (u16*)k_cache, (u16*)v_cache};
+  attn_decode_k<128, true><<<dim3(nchunk, H, B), 256, 0, s>>>((const u16*)q, ldq, (const u16*)k_cache,
+                                                              (const u16*)v_cache, ld_tok, ld_batch, nullptr,
+                                                              kv_start, scale * kLog2e, part_o, part_ml, H, nchunk, rp);
+  attn_decode_combine_k<128><<<dim3(H, B), 128, 0, s>>>(part_o, part_ml, (u16*)o, ldo, H, nchunk);
+  return cullavo_check_launch("attn_decode_rope");
 }
 
 extern "C" int cullavo_attn_decode(const void* q, int64_t ldq, const void* k_cache, const void* v_cache,

@@ -67,20 +67,31 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, f
 // 4 fits 4, so one workgroup's ramp / reduction runs under the others' streams.
 // NW: waves per workgroup (K split NW ways); 16 for the N = 4096 products, whose 256 workgroups
 // are one per CU whatever the occupancy allows
-template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves>
+// OT: output transform. 0 none; 1 SwiGLU of the product (cullavo_decode_linear transform 3): B
+// holds 2N rows (gate rows [0, N), up rows [N, 2N), the fused gate|up weight) and the workgroup's
+// 16 MFMA rows are 8 gate rows and the matching 8 up rows, so each lane pair (l, l + 32) holds
+// g and u of one output: y = bf16(bf16(silu(g)) * u) with g, u first rounded to bf16 as the
+// unfused product stores them -- bitwise swiglu_fwd_k of that product, without its launch or the
+// [M, 2N] round trip.
+template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves, int OT = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : NBW >= 8 ? 4 : 8))) void gemv_k(GemvArgs a) {
+  static_assert(OT == 0 || RB == 1, "SwiGLU pairing: one 16-row block per workgroup");
   const GemmArgs& p = a.g;
   __shared__ f32x4 red[NW][RB][64];
   __shared__ float rs[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n0 = (int64_t)blockIdx.x * 16 * RB;
+  const int64_t n0 = (int64_t)blockIdx.x * (OT == 1 ? 8 : 16 * RB);
   const int64_t nk = cdiv(p.K, 32);
   const int64_t per = cdiv(nk, NW);
   const int r = lane & 15, g = lane >> 4;
   const u16* wrow[RB];
+  if constexpr (OT == 1) {
+    wrow[0] = p.B + (min(n0 + (r & 7), p.N - 1) + (r >= 8 ? p.N : 0)) * p.ldb + 8 * g;
+  } else {
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb) wrow[rb] = p.B + min(n0 + 16 * rb + r, p.N - 1) * p.ldb + 8 * g;
+    for (int rb = 0; rb < RB; ++rb) wrow[rb] = p.B + min(n0 + 16 * rb + r, p.N - 1) * p.ldb + 8 * g;
+  }
   const bool xrow = r < p.M;
   const u16* xp = p.A + (xrow ? r : 0) * p.lda + 8 * g;
   float rstd = 0.f;
@@ -154,7 +165,20 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
     f32x4 s = red[0][wave][lane];
 #pragma unroll
     for (int w2 = 1; w2 < NW; ++w2) s += red[w2][wave][lane];
-    store4<CT>(p, s, r, n0 + 16 * wave + 4 * g);
+    if constexpr (OT == 1) {
+      // lanes 0-31 hold g of outputs n0 + 4 (lane >> 4) + j, lanes 32-63 the matching u
+      f32x4 u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u[j] = __shfl_xor(s[j], 32);
+      if (g < 2 && r < p.M) {
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = f2bf(round_bf(gemv_silu(round_bf(s[j]))) * round_bf(u[j]));
+        *reinterpret_cast<u16x4*>(reinterpret_cast<u16*>(p.C) + r * p.ldc + n0 + 4 * g) = o;
+      }
+    } else {
+      store4<CT>(p, s, r, n0 + 16 * wave + 4 * g);
+    }
   }
 }
 
@@ -192,7 +216,8 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
 extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
                                      const void* norm_w, float eps, const void* W, int64_t ldw, void* y,
                                      int64_t ldy, const void* residual, int64_t ldr, void* stream) {
-  CV_REQUIRE(x_transform >= 0 && x_transform <= 2, CULLAVO_EINVAL, "decode_linear: x_transform 0, 1 or 2");
+  CV_REQUIRE(x_transform >= 0 && x_transform <= 3, CULLAVO_EINVAL, "decode_linear: transform 0, 1, 2 or 3");
+  CV_REQUIRE(x_transform != 3 || residual == nullptr, CULLAVO_EINVAL, "decode_linear: transform 3 takes no residual");
   CV_REQUIRE(M >= 1 && M <= 16 && N > 0 && K > 0, CULLAVO_EINVAL, "decode_linear: 1 <= M <= 16 rows, N, K > 0");
   CV_REQUIRE(N % 8 == 0 && K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldy % 8 == 0 &&
                  (residual == nullptr || ldr % 8 == 0),
@@ -214,15 +239,19 @@ extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int6
   p.act = CULLAVO_ACT_NONE;
   a.xf_w = (const u16*)norm_w;
   a.xf_eps = eps;
-  const unsigned grid = (unsigned)cdiv(N, 16);
+  const unsigned grid = (unsigned)cdiv(N, x_transform == 3 ? 8 : 16);
   // the shapes' variants as cvgemm_launch_gemv picks them: 16 waves x 4-load batches for the widest
-  // products, 4-load batches for K >= 8192, else 8-load batches
-  const int v = K >= 8192 ? 6 : N > 16384 ? 8 : kGemvDefault;
+  // products, 4-load batches for K >= 8192, else 8-load batches (transform 3: the 2N-row product)
+  const int64_t wrows = x_transform == 3 ? 2 * N : N;
+  const int v = K >= 8192 ? 6 : wrows > 16384 ? 8 : kGemvDefault;
 #define DL(XF)                                                                                        \
   if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16><<<grid, 64 * 16, 0, s>>>(a);                      \
   else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4><<<grid, 64 * kGemvWaves, 0, s>>>(a);             \
   else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  if (x_transform == 0) { DL(0) } else if (x_transform == 1) { DL(1) } else { DL(2) }
+  if (x_transform == 0) { DL(0) } else if (x_transform == 1) { DL(1) } else if (x_transform == 2) { DL(2) }
+  else if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 4, 16, 1><<<grid, 64 * 16, 0, s>>>(a);
+  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 4, kGemvWaves, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 8, kGemvWaves, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
 #undef DL
   return cullavo_check_launch("decode_linear");
 }

@@ -26,12 +26,18 @@ from .lora import NO_LORA
 
 import os
 
-# decode-step fusions into the weight-streaming products (cullavo_decode_linear): "norm" folds the
-# two RMSNorms into the q|k|v and gate|up products' X loads, "swiglu" the SwiGLU into down_proj's
-# (both bitwise the unfused values); CULLAVO_DECODE_FUSE="norm,swiglu" / "norm" / "" (none)
-_FUSE = {f.strip() for f in os.environ.get("CULLAVO_DECODE_FUSE", "").split(",") if f.strip()}
+# decode-step fusions (all bitwise the unfused values), CULLAVO_DECODE_FUSE = comma list:
+#   "gu"    (default on) the SwiGLU in the gate|up product's epilogue (cullavo_decode_linear
+#           transform 3: one launch instead of the product + cullavo_swiglu_fwd);
+#   "rope"  (default on) RoPE + KV append inside decode attention (cullavo_attn_decode_rope);
+#   "norm"  the two RMSNorms into the q|k|v and gate|up products' X loads, "swiglu" the SwiGLU into
+#           down_proj's X loads (measured ~2x slower per product, profiles/r04/decode/decode_fusions_ab.txt:
+#           off by default)
+_FUSE = {f.strip() for f in os.environ.get("CULLAVO_DECODE_FUSE", "gu,rope").split(",") if f.strip()}
 FUSE_DECODE_NORMS = "norm" in _FUSE
 FUSE_DECODE_SWIGLU = "swiglu" in _FUSE
+FUSE_DECODE_GU = "gu" in _FUSE
+FUSE_DECODE_ROPE = "rope" in _FUSE
 
 
 class KVCache:
@@ -139,7 +145,12 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
         t, _ = lg["qkv"].forward(x1, False, 0)
         qkv = ops.linear(x1, layer.w_qkv(), addend=t)
     q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
-    if Lnew == 1 and qkv.dtype == torch.bfloat16:
+    if Lnew == 1 and qkv.dtype == torch.bfloat16 and FUSE_DECODE_ROPE:
+        # decode: RoPE, the cache append and attention in one pass (the cache row is start[b])
+        o = ops.attn_decode_rope(q, k, v, sctx.position_ids, cache.k[li], cache.v[li], start, B=B, H=H, D=D,
+                                 max_len=attn_len if attn_len is not None else cache.length + 1,
+                                 scale=D ** -0.5, theta=cfg.rope_theta, kv_start=sctx.kv_start)
+    elif Lnew == 1 and qkv.dtype == torch.bfloat16:
         # decode: rotated k goes straight to the cache (one launch for RoPE + append)
         ops.rope_kv_append(q, k, v, sctx.position_ids, cache.k[li], cache.v[li], start, hq=H, head_dim=D,
                            theta=cfg.rope_theta, B=B, Lnew=1)
@@ -149,7 +160,7 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     if Lnew > 1:
         o, _ = ops.attn_fwd(q, k, v, B=B, H=H, Lq=Lnew, Lk=Lnew, D=D, scale=D ** -0.5, causal=True,
                             kv_start=sctx.kv_start)
-    else:
+    elif not (qkv.dtype == torch.bfloat16 and FUSE_DECODE_ROPE):
         o = ops.attn_decode(q, cache.k[li], cache.v[li], kv_len, B=B, H=H, D=D,
                             max_len=attn_len if attn_len is not None else cache.length + 1,
                             scale=D ** -0.5, kv_start=sctx.kv_start)
@@ -163,8 +174,11 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
         return ops.linear(ops.swiglu_fwd(gu), layer.mlp.down_proj.weight, residual=h2)
     x2, _ = ops.rmsnorm_fwd(h2, layer.post_attention_layernorm.weight, cfg.rms_norm_eps)
     t, _ = lg["gu"].forward(x2, False, 0)
-    gu = ops.linear(x2, layer.w_gu(), addend=t)
-    a = ops.swiglu_fwd(gu)
+    if FUSE_DECODE_GU and t is None and Lnew == 1 and x2.shape[0] <= 16 and x2.dtype == torch.bfloat16:
+        a = ops.decode_linear(x2, layer.w_gu(), transform=3)  # gate|up product + SwiGLU, one launch
+    else:
+        gu = ops.linear(x2, layer.w_gu(), addend=t)
+        a = ops.swiglu_fwd(gu)
     t, _ = lg["down"].forward(a, False, 0)
     return ops.linear(a, layer.mlp.down_proj.weight, residual=h2, addend=t)
 

@@ -345,10 +345,13 @@ def swiglu_fwd(gu):
 
 def decode_linear(x, w, *, transform: int = 0, norm_w=None, eps: float = 0.0, residual=None):
     """Decode rows (M <= 16) through cullavo_decode_linear: y = T(x) @ w.T (+ residual) with T the
-    fused input transform (0 none, 1 RMSNorm with norm_w / eps, 2 SwiGLU of x = gate|up [M, 2K])."""
+    fused input transform (0 none, 1 RMSNorm with norm_w / eps, 2 SwiGLU of x = gate|up [M, 2K]);
+    transform 3: y = SwiGLU(x @ w.T) for the fused gate|up weight w [2N, K] (y [M, N])."""
     _dev(x, w, norm_w, residual)
     M = x.shape[0]
     N, K = w.shape
+    if transform == 3:
+        N //= 2
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     call("decode_linear", int(transform), M, N, K, _ptr(x), _ld(x), _ptr(norm_w), float(eps), _ptr(w), _ld(w),
          _ptr(y), _ld(y), _ptr(residual), _ld(residual) if residual is not None else 0, _stream())
@@ -415,6 +418,21 @@ def kv_append(k, v, k_cache, v_cache, start, *, B: int, Lnew: int):
     hd = k_cache.shape[-1]
     call("kv_append", _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(k_cache), _ptr(v_cache), k_cache.stride(1),
          k_cache.stride(0), _ptr(start), B, Lnew, hd, _stream())
+
+
+def attn_decode_rope(q, k, v, position_ids, k_cache, v_cache, start, *, B: int, H: int, D: int, max_len: int,
+                     scale: float, theta: float, kv_start=None, out=None):
+    """cullavo_attn_decode_rope: rope_kv_append (Lnew = 1) + attn_decode over keys
+    [kv_start, start + 1) in one pass; q, k, v the unrotated projection rows [B, >=H*D] (q is left
+    unrotated), the rotated key and the value written to cache row start[b]."""
+    _dev(q, k, v, position_ids, k_cache, v_cache, start, kv_start)
+    o = out if out is not None else torch.empty((B, H * D), dtype=q.dtype, device=q.device)
+    nbytes = lib().cullavo_attn_decode_workspace(B, H, max_len, D)
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+    call("attn_decode_rope", _ptr(q), _ld(q), _ptr(k), _ld(k), _ptr(v), _ld(v), _ptr(position_ids), float(theta),
+         _ptr(k_cache), _ptr(v_cache), k_cache.stride(1), k_cache.stride(0), _ptr(start), _ptr(kv_start), _ptr(o),
+         _ld(o), B, H, max_len, D, float(scale), _ptr(ws), _stream())
+    return o
 
 
 def attn_decode(q, k_cache, v_cache, kv_len, *, B: int, H: int, D: int, max_len: int, scale: float,

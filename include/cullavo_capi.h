@@ -326,6 +326,15 @@ int cullavo_attn_set_rescale(float threshold, float* previous);
  * against cache keys kv_start[b] <= key < kv_len[b] (kv_start nullable); max_len >= every
  * kv_len sizes the split over keys; workspace: cullavo_attn_decode_workspace bytes (f32).
  * A row with no visible key returns zeros (as the training kernel's fully masked rows). */
+/* One decode step's RoPE + KV append + attention in one pass (ABI 4, additive): bitwise
+ * cullavo_rope_kv_append(q, k, v, position_ids, ..., Lnew = 1) followed by cullavo_attn_decode
+ * with kv_len = start + 1, except that q (the unrotated projection row, [B, >=H*D]) is only read:
+ * the rotated key and the value of row start[b] are written to the caches, every chunk rotates its
+ * query itself. Workspace: cullavo_attn_decode_workspace(B, H, max_len, D) bytes. */
+int cullavo_attn_decode_rope(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                             const int64_t* position_ids, float theta, void* k_cache, void* v_cache, int64_t ld_tok,
+                             int64_t ld_batch, const int32_t* start, const int32_t* kv_start, void* o, int64_t ldo,
+                             int B, int H, int max_len, int D, float scale, float* workspace, void* stream);
 int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, void* k_cache, void* v_cache,
                       int64_t ld_tok, int64_t ld_batch, const int32_t* start, int B, int Lnew, int64_t hd,
                       void* stream);
@@ -336,6 +345,9 @@ int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, vo
  *   1: RMSNorm(x; norm_w, eps) of x [M,K] (the residual stream: replaces cullavo_rmsnorm_fwd
  *      + cullavo_gemm, the values bitwise those of cullavo_rmsnorm_fwd);
  *   2: SwiGLU of x = gate|up [M,2K] (replaces cullavo_swiglu_fwd + cullavo_gemm, bitwise).
+ * x_transform 3 transforms the OUTPUT instead: W holds 2N rows (gate rows, then up rows: the
+ *   fused gate|up weight [2N, K]) and y[M,N] = SwiGLU(x W^T), i.e. cullavo_gemm's bf16 gate|up
+ *   product followed by cullavo_swiglu_fwd, bitwise, in one launch (no residual).
  * bf16 only; the result is rounded like cullavo_gemm's (residual added after rounding). */
 int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
                           const void* norm_w, float eps, const void* W, int64_t ldw, void* y, int64_t ldy,

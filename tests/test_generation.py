@@ -376,3 +376,77 @@ def test_rope_kv_append_bitwise(Lnew):
     torch.cuda.synchronize()
     assert torch.equal(a[:, :d], b2[:, :d])
     assert torch.equal(ka, kb) and torch.equal(va, vb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,F,K", [(1, 11008, 4096), (3, 264, 1000), (8, 11008, 4096), (16, 776, 520)])
+def test_decode_linear_swiglu_output_bitwise(M, F, K):
+    """cullavo_decode_linear transform 3 (the gate|up product with the SwiGLU in its epilogue, the
+    decode step's default) is bitwise swiglu_fwd(gate|up product) of the unfused path."""
+    import torch
+    from cullavo_amd import ops
+    g = torch.Generator().manual_seed(M + F)
+    x = torch.randn(M, K, generator=g).bfloat16().cuda()
+    w = (torch.randn(2 * F, K, generator=g) * K ** -0.5).bfloat16().cuda()
+    ref = ops.swiglu_fwd(ops.gemm_ex(0, 0, M, 2 * F, K, x, K, w, K, torch.empty(M, 2 * F, dtype=torch.bfloat16,
+                                                                                  device="cuda"), 2 * F))
+    out = ops.decode_linear(x, w, transform=3)
+    torch.cuda.synchronize()
+    assert out.shape == (M, F)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("starts", [(3, 0, 17), (63, 64, 127), (1100, 5, 640)])
+def test_attn_decode_rope_bitwise(starts):
+    """cullavo_attn_decode_rope (RoPE + cache append + split-KV attention in one pass, the decode
+    step's default) gives bitwise the output and cache rows of rope_kv_append + attn_decode with
+    kv_len = start + 1: new rows at chunk edges (63 / 64 / 127), left padding (kv_start), a
+    max_len past every length (empty chunks), q left unrotated."""
+    import torch
+    from cullavo_amd import ops
+    B, H, D = 3, 4, 128
+    d = H * D
+    Lmax = max(starts) + 70
+    g = torch.Generator().manual_seed(sum(starts))
+    qkv = torch.randn(B, 3 * d, generator=g).bfloat16().cuda()
+    pos = torch.tensor([s + 2 for s in starts], dtype=torch.int64).cuda()
+    start = torch.tensor(starts, dtype=torch.int32).cuda()
+    kv_start = torch.tensor([0, min(starts[1], 2), 1], dtype=torch.int32).cuda()
+    caches = [torch.randn(B, Lmax, d, generator=g).bfloat16().cuda() for _ in range(2)]
+    a = qkv.clone()
+    ka, va = caches[0].clone(), caches[1].clone()
+    ops.rope_kv_append(a[:, :d], a[:, d:2 * d], a[:, 2 * d:], pos, ka, va, start, hq=H, head_dim=D, theta=10000.0,
+                       B=B, Lnew=1)
+    oa = ops.attn_decode(a[:, :d], ka, va, start + 1, B=B, H=H, D=D, max_len=Lmax, scale=D ** -0.5, kv_start=kv_start)
+    b2 = qkv.clone()
+    kb, vb = caches[0].clone(), caches[1].clone()
+    ob = ops.attn_decode_rope(b2[:, :d], b2[:, d:2 * d], b2[:, 2 * d:], pos, kb, vb, start, B=B, H=H, D=D,
+                              max_len=Lmax, scale=D ** -0.5, theta=10000.0, kv_start=kv_start)
+    torch.cuda.synchronize()
+    assert torch.equal(b2, qkv)  # q, k, v read only
+    assert torch.equal(ka, kb) and torch.equal(va, vb)
+    assert torch.equal(oa, ob)
+
+
+@pytest.mark.gpu
+def test_decode_default_fusions_bitwise(monkeypatch):
+    """The default decode fusions (SwiGLU in the gate|up product's epilogue, RoPE + append inside
+    decode attention) give bitwise the logits of the separate kernels, eager and graph-replayed."""
+    from cullavo_amd import generation
+    cfg = O.config_small_gpu()
+    m = _model(6)
+    ids, mask, pix, _ = O.make_inputs(cfg, 2, 20, 3, 31)
+    ids, mask, pix = ids.cuda(), mask.cuda(), pix.cuda()
+    toks = torch.randint(2, cfg.image_token_index, (4, 2), generator=torch.Generator().manual_seed(9)).cuda()
+    runs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(generation, "FUSE_DECODE_GU", fuse)
+        monkeypatch.setattr(generation, "FUSE_DECODE_ROPE", fuse)
+        cache = m(input_ids=ids, pixel_values=pix, attention_mask=mask, use_cache=True).past_key_values
+        runs.append([m(input_ids=t[:, None], past_key_values=cache, use_cache=True).logits.clone() for t in toks])
+        kw = dict(input_ids=ids, pixel_values=pix, attention_mask=mask, max_new_tokens=5)
+        runs.append([m.generate(**kw)])
+    for i, (a, b) in enumerate(zip(runs[0], runs[2])):
+        assert torch.equal(a, b), i
+    assert torch.equal(runs[1][0], runs[3][0])
