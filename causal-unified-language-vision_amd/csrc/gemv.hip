@@ -41,15 +41,12 @@ struct GemvArgs {
 };
 
 template <int XF>
-DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, float rstd) {
+DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, const u16* xs_row) {
+  if (XF == 1) return __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(xs_row + k));  // normalised, LDS
   const u16x8 xv = *reinterpret_cast<const u16x8*>(xp + off);
   if (XF == 0) return __builtin_bit_cast(frag8, xv);
   u16x8 o;
-  if (XF == 1) {
-    const u16x8 wv = *reinterpret_cast<const u16x8*>(a.xf_w + k);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wv[j]) * round_bf(bf2f(xv[j]) * rstd));
-  } else {
+  {
     const u16x8 uv = *reinterpret_cast<const u16x8*>(xp + off + a.g.K);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f2bf(round_bf(gemv_silu(bf2f(xv[j]))) * bf2f(uv[j]));
@@ -78,7 +75,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
   static_assert(OT == 0 || RB == 1, "SwiGLU pairing: one 16-row block per workgroup");
   const GemmArgs& p = a.g;
   __shared__ f32x4 red[NW][RB][64];
-  __shared__ float rs[16];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n0 = (int64_t)blockIdx.x * (OT == 1 ? 8 : 16 * RB);
@@ -94,7 +90,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
   }
   const bool xrow = r < p.M;
   const u16* xp = p.A + (xrow ? r : 0) * p.lda + 8 * g;
-  float rstd = 0.f;
+  // XF 1: the M normalised rows [M][K + 8] in LDS (dynamic; row pad 16 B: the fragment reads of
+  // rows r and r + 1 fall on different banks)
+  extern __shared__ __attribute__((aligned(16))) u16 xs[];
+  const int64_t xs_ld = p.K + 8;
+  const u16* xs_row = xs + (xrow ? r : 0) * xs_ld;
   f32x4 acc[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -113,23 +113,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
         w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
     }
     if (XF == 1 && j0 == 0) {
-      // RMSNorm row statistics, after the first batch of weight loads is in flight: rmsnorm_fwd_k's
-      // arithmetic (one wave per row, the same summation order), handed over through LDS with a
-      // barrier that waits on the LDS only (the weight loads stay in flight)
+      // RMSNorm of the M rows, after the first batch of weight loads is in flight: rmsnorm_fwd_k's
+      // arithmetic (one wave per row, the same summation order, y = w * rnd(x * rstd)) written
+      // once into LDS, handed over with a barrier that waits on the LDS only (the weight loads stay
+      // in flight); every later x fragment is an LDS read
       for (int row = wave; row < p.M; row += NW) {
         const u16* xr = p.A + row * p.lda;
         float ss = 0.f;
-        // 8 row loads in flight per round (one round at K = 4096): a load-use loop here costs a
-        // memory round trip per 512 columns, which every wave of the workgroup waits for
-        for (int c0 = 0; c0 * 512 < p.K; c0 += 8) {
-          u16x8 xv[8];
+        // 2 row loads in flight per round (more spilled the 4- and 8-load variants, whose
+        // waves_per_eu caps them at 64 / 128 registers: the round-4 form with 8 in flight ran the
+        // products 2-3x slower out of scratch); the accumulation order (chunk, then element) is
+        // rmsnorm_fwd_k's whatever the batching
+        for (int c0 = 0; c0 * 512 < p.K; c0 += 2) {
+          u16x8 xv[2];
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
+          for (int c = 0; c < 2; ++c) {
             const int col = (c0 + c) * 512 + lane * 8;
             xv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(xr + col) : u16x8{};
           }
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
+          for (int c = 0; c < 2; ++c) {
             const int col = (c0 + c) * 512 + lane * 8;
             if (col < p.K) {
 #pragma unroll
@@ -138,11 +141,29 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
           }
         }
         ss = wave_sum(ss);
-        if (lane == 0) rs[row] = rsqrtf(ss / (float)p.K + a.xf_eps);
+        const float rr = rsqrtf(ss / (float)p.K + a.xf_eps);
+        for (int c0 = 0; c0 * 512 < p.K; c0 += 2) {
+          u16x8 xv[2], wv[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int col = (c0 + c) * 512 + lane * 8;
+            xv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(xr + col) : u16x8{};
+            wv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(a.xf_w + col) : u16x8{};
+          }
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int col = (c0 + c) * 512 + lane * 8;
+            if (col < p.K) {
+              u16x8 o;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wv[c][j]) * round_bf(bf2f(xv[c][j]) * rr));
+              *reinterpret_cast<u16x8*>(xs + row * xs_ld + col) = o;
+            }
+          }
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      rstd = xrow ? rs[r] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -151,7 +172,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
       const int64_t k = ks * 32 + 8 * g;
       const bool in = j0 + i < per && ks < kend && k < p.K;
       const int64_t off = in ? ks * 32 : 0;
-      x[i] = (in && xrow) ? gemv_xfrag<XF>(a, xp, off, k, rstd) : frag8{};
+      x[i] = (in && xrow) ? gemv_xfrag<XF>(a, xp, off, k, xs_row) : frag8{};
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
@@ -216,16 +237,19 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
 extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
                                      const void* norm_w, float eps, const void* W, int64_t ldw, void* y,
                                      int64_t ldy, const void* residual, int64_t ldr, void* stream) {
-  CV_REQUIRE(x_transform >= 0 && x_transform <= 3, CULLAVO_EINVAL, "decode_linear: transform 0, 1, 2 or 3");
-  CV_REQUIRE(x_transform != 3 || residual == nullptr, CULLAVO_EINVAL, "decode_linear: transform 3 takes no residual");
+  CV_REQUIRE(x_transform >= 0 && x_transform <= 4, CULLAVO_EINVAL, "decode_linear: transform 0 to 4");
+  const int xf = (x_transform == 1 || x_transform == 4) ? 1 : x_transform == 2 ? 2 : 0;
+  const bool ot = x_transform == 3 || x_transform == 4;
+  CV_REQUIRE(!ot || residual == nullptr, CULLAVO_EINVAL, "decode_linear: the SwiGLU output takes no residual");
   CV_REQUIRE(M >= 1 && M <= 16 && N > 0 && K > 0, CULLAVO_EINVAL, "decode_linear: 1 <= M <= 16 rows, N, K > 0");
   CV_REQUIRE(N % 8 == 0 && K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldy % 8 == 0 &&
                  (residual == nullptr || ldr % 8 == 0),
              CULLAVO_EINVAL, "decode_linear: sizes and strides must be multiples of 8");
-  CV_REQUIRE(ldw >= K && ldy >= N && ldx >= (x_transform == 2 ? 2 * K : K) && (residual == nullptr || ldr >= N),
+  CV_REQUIRE(ldw >= K && ldy >= N && ldx >= (xf == 2 ? 2 * K : K) && (residual == nullptr || ldr >= N),
              CULLAVO_EINVAL, "decode_linear: leading dimension too small");
-  CV_REQUIRE(x_transform != 1 || (norm_w != nullptr && K <= 8192), CULLAVO_EINVAL,
-             "decode_linear: RMSNorm needs its weight and K <= 8192");
+  // the normalised rows live in LDS: M (K + 8) bf16 <= 64 KiB (M <= 7 at K = 4096)
+  CV_REQUIRE(xf != 1 || (norm_w != nullptr && M * (K + 8) * 2 <= 65536), CULLAVO_EINVAL,
+             "decode_linear: RMSNorm needs its weight and M * (K + 8) * 2 <= 65536");
   hipStream_t s = CV_STREAM(stream);
   GemvArgs a{};
   GemmArgs& p = a.g;
@@ -239,19 +263,18 @@ extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int6
   p.act = CULLAVO_ACT_NONE;
   a.xf_w = (const u16*)norm_w;
   a.xf_eps = eps;
-  const unsigned grid = (unsigned)cdiv(N, x_transform == 3 ? 8 : 16);
+  const unsigned grid = (unsigned)cdiv(N, ot ? 8 : 16);
+  const size_t smem = xf == 1 ? (size_t)M * (K + 8) * 2 : 0;
   // the shapes' variants as cvgemm_launch_gemv picks them: 16 waves x 4-load batches for the widest
-  // products, 4-load batches for K >= 8192, else 8-load batches (transform 3: the 2N-row product)
-  const int64_t wrows = x_transform == 3 ? 2 * N : N;
+  // products, 4-load batches for K >= 8192, else 8-load batches (SwiGLU output: the 2N-row product)
+  const int64_t wrows = ot ? 2 * N : N;
   const int v = K >= 8192 ? 6 : wrows > 16384 ? 8 : kGemvDefault;
-#define DL(XF)                                                                                        \
-  if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16><<<grid, 64 * 16, 0, s>>>(a);                      \
-  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4><<<grid, 64 * kGemvWaves, 0, s>>>(a);             \
-  else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  if (x_transform == 0) { DL(0) } else if (x_transform == 1) { DL(1) } else if (x_transform == 2) { DL(2) }
-  else if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 4, 16, 1><<<grid, 64 * 16, 0, s>>>(a);
-  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 4, kGemvWaves, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
-  else gemv_k<CULLAVO_DT_BF16, 0, 1, 0, 8, kGemvWaves, 1><<<grid, 64 * kGemvWaves, 0, s>>>(a);
+#define DL(XF, OT)                                                                                          \
+  if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16, OT><<<grid, 64 * 16, smem, s>>>(a);                   \
+  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, kGemvWaves, OT><<<grid, 64 * kGemvWaves, smem, s>>>(a); \
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8, kGemvWaves, OT><<<grid, 64 * kGemvWaves, smem, s>>>(a);
+  if (x_transform == 0) { DL(0, 0) } else if (x_transform == 1) { DL(1, 0) } else if (x_transform == 2) { DL(2, 0) }
+  else if (x_transform == 3) { DL(0, 1) } else { DL(1, 1) }
 #undef DL
   return cullavo_check_launch("decode_linear");
 }

@@ -130,12 +130,12 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     d, H, D = cfg.hidden_size, cfg.num_attention_heads, cfg.head_dim
     lg = layer.lora_groups
     B = sctx.B
-    # FUSE_DECODE_NORMS / _SWIGLU: the norms and the SwiGLU inside the weight-streaming products
-    # (cullavo_decode_linear transforms 1 / 2, bitwise the unfused values) -- measured ~2x slower per
-    # product than the separate kernels: a workgroup streams only two weight batches, and the row
-    # statistics (or the SwiGLU) put a dependent memory round trip in front of its first MFMA (7B step
-    # 7.01 / 7.81 vs 3.69 ms at batch 1, profiles/r04/decode/decode_fusions_ab.txt), so off
-    fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] <= 16 and h.dtype == torch.bfloat16
+    # FUSE_DECODE_NORMS: the RMSNorms inside the q|k|v and gate|up weight-streaming products
+    # (cullavo_decode_linear transform 1 / 4: every workgroup normalises the rows once into LDS; the
+    # round-4 per-fragment form was ~2x slower, profiles/r04/decode/decode_fusions_ab.txt) for the
+    # rows that fit LDS (M (d + 8) * 2 <= 64 KiB); FUSE_DECODE_SWIGLU: the SwiGLU in down_proj's
+    # X loads (transform 2), only without FUSE_DECODE_GU. All bitwise the unfused values.
+    fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] * (d + 8) * 2 <= 65536 and h.dtype == torch.bfloat16
              and all(g is NO_LORA for g in lg.values()))
     if fused:
         qkv = ops.decode_linear(h, layer.w_qkv(), transform=1, norm_w=layer.input_layernorm.weight,
@@ -167,6 +167,10 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     t, _ = lg["o"].forward(o, False, 0)
     h2 = ops.linear(o, layer.self_attn.o_proj.weight, residual=h, addend=t)
     if fused:
+        if FUSE_DECODE_GU:  # RMSNorm, gate|up product and SwiGLU in one launch (transform 4)
+            a = ops.decode_linear(h2, layer.w_gu(), transform=4, norm_w=layer.post_attention_layernorm.weight,
+                                  eps=cfg.rms_norm_eps)
+            return ops.linear(a, layer.mlp.down_proj.weight, residual=h2)
         gu = ops.decode_linear(h2, layer.w_gu(), transform=1, norm_w=layer.post_attention_layernorm.weight,
                                eps=cfg.rms_norm_eps)
         if FUSE_DECODE_SWIGLU:
@@ -224,7 +228,8 @@ class DecodeGraph:
         B = cache.B
         h = self.embed(self.ids[:, None]).reshape(B, cfg.hidden_size)
         sctx = StepContext(B, 1, self.pos[:, None], cache.kv_start, lora_seed=0)
-        kv_len = self.start + 1
+        # the unfused decode attention reads kv_len = start + 1 (the fused one derives it from start)
+        kv_len = None if FUSE_DECODE_ROPE and cache.k.dtype == torch.bfloat16 else self.start + 1
         for li, layer in enumerate(lm.model.layers):
             h = layer_infer(layer, h, sctx, cache, li, 1, self.start, kv_len, attn_len=cache.max_len)
         x, _ = ops.rmsnorm_fwd(h, lm.model.norm.weight, cfg.rms_norm_eps)

@@ -346,11 +346,11 @@ def swiglu_fwd(gu):
 def decode_linear(x, w, *, transform: int = 0, norm_w=None, eps: float = 0.0, residual=None):
     """Decode rows (M <= 16) through cullavo_decode_linear: y = T(x) @ w.T (+ residual) with T the
     fused input transform (0 none, 1 RMSNorm with norm_w / eps, 2 SwiGLU of x = gate|up [M, 2K]);
-    transform 3: y = SwiGLU(x @ w.T) for the fused gate|up weight w [2N, K] (y [M, N])."""
+    transform 3: y = SwiGLU(x @ w.T) for the fused gate|up weight w [2N, K] (y [M, N]); 4: 1 and 3."""
     _dev(x, w, norm_w, residual)
     M = x.shape[0]
     N, K = w.shape
-    if transform == 3:
+    if transform in (3, 4):
         N //= 2
     y = torch.empty((M, N), dtype=x.dtype, device=x.device)
     call("decode_linear", int(transform), M, N, K, _ptr(x), _ld(x), _ptr(norm_w), float(eps), _ptr(w), _ld(w),

@@ -343,11 +343,13 @@ int cullavo_kv_append(const void* k, int64_t ldk, const void* v, int64_t ldv, vo
  * stream (csrc/gemv.hip): y[M,N] = X W^T (+ residual), W [N,K] bf16 (ldw), where X is
  *   x_transform 0: x [M,K] as given;
  *   1: RMSNorm(x; norm_w, eps) of x [M,K] (the residual stream: replaces cullavo_rmsnorm_fwd
- *      + cullavo_gemm, the values bitwise those of cullavo_rmsnorm_fwd);
+ *      + cullavo_gemm, the values bitwise those of cullavo_rmsnorm_fwd; every workgroup normalises
+ *      the rows once into LDS, so M (K + 8) * 2 <= 65536 bytes);
  *   2: SwiGLU of x = gate|up [M,2K] (replaces cullavo_swiglu_fwd + cullavo_gemm, bitwise).
  * x_transform 3 transforms the OUTPUT instead: W holds 2N rows (gate rows, then up rows: the
  *   fused gate|up weight [2N, K]) and y[M,N] = SwiGLU(x W^T), i.e. cullavo_gemm's bf16 gate|up
- *   product followed by cullavo_swiglu_fwd, bitwise, in one launch (no residual).
+ *   product followed by cullavo_swiglu_fwd, bitwise, in one launch (no residual);
+ *   4 = 1 and 3 together: SwiGLU(RMSNorm(x) W^T).
  * bf16 only; the result is rounded like cullavo_gemm's (residual added after rounding). */
 int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int64_t K, const void* x, int64_t ldx,
                           const void* norm_w, float eps, const void* W, int64_t ldw, void* y, int64_t ldy,

@@ -330,9 +330,14 @@ def test_decode_linear_fused_transforms_bitwise(M):
     Wd = (torch.randn(d, F, generator=g) * F ** -0.5).to(BF).cuda()
     res = torch.randn(M, d, generator=g).to(BF).cuda()
     x1, _ = ops.rmsnorm_fwd(h, nw, 1e-5)
-    a = ops.decode_linear(h, Wq, transform=1, norm_w=nw, eps=1e-5)
-    b = ops.decode_linear(x1, Wq)
-    assert torch.equal(a, b)
+    norm_fits = M * (d + 8) * 2 <= 65536  # the normalised rows are staged in LDS
+    if norm_fits:
+        a = ops.decode_linear(h, Wq, transform=1, norm_w=nw, eps=1e-5)
+        b = ops.decode_linear(x1, Wq)
+        assert torch.equal(a, b)
+    else:
+        with pytest.raises(ValueError):
+            ops.decode_linear(h, Wq, transform=1, norm_w=nw, eps=1e-5)
     act = ops.swiglu_fwd(gu)
     for r in (None, res):
         a = ops.decode_linear(gu, Wd, transform=2, residual=r)
@@ -340,8 +345,12 @@ def test_decode_linear_fused_transforms_bitwise(M):
         assert torch.equal(a, b)
     # the widest product (gate|up: 16-wave workgroups) and the plain linear's dispatch agree too
     Wgu = (torch.randn(2 * F, d, generator=g) * d ** -0.5).to(BF).cuda()
-    a = ops.decode_linear(h, Wgu, transform=1, norm_w=nw, eps=1e-5)
-    assert torch.equal(a, ops.linear(x1, Wgu))
+    if norm_fits:
+        a = ops.decode_linear(h, Wgu, transform=1, norm_w=nw, eps=1e-5)
+        assert torch.equal(a, ops.linear(x1, Wgu))
+        # RMSNorm in, SwiGLU out (transform 4): the whole gate|up half of the decode MLP
+        a = ops.decode_linear(h, Wgu, transform=4, norm_w=nw, eps=1e-5)
+        assert torch.equal(a, ops.swiglu_fwd(ops.linear(x1, Wgu)))
     assert torch.equal(ops.decode_linear(act, Wd, residual=res), ops.linear(act, Wd, residual=res))
     z = x1.float() @ Wq.float().T
     y = ops.decode_linear(x1, Wq)
