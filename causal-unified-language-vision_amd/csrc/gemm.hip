@@ -385,7 +385,10 @@ double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 // on that tile and the remaining rows as a second, thin product (128x128 tiles, split over K
 // when the caller gives the workspace), if that is estimated at least 5 % faster.
 int g_msplit = 1;
-double rem_seconds(int64_t rows, int64_t N, int64_t K) { return 2.0 * rows * N * K / 200e12 + 6e-6; }
+// the thin product's time: its split-K launch + reduce cost 16-19 us at the ViT shapes (64 rows:
+// profiles/r05/vit/vit_kernel_trace.txt), so a split pays only where it saves more than that --
+// fc2 (K = 4096: 3 -> 2 rounds of 288-row tiles), not fc1 / o (K = 1024)
+double rem_seconds(int64_t rows, int64_t N, int64_t K) { return 2.0 * rows * N * K / 150e12 + 16e-6; }
 
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_t* m_main = nullptr) {
   if (m_main) *m_main = 0;

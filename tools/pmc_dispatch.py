@@ -61,7 +61,7 @@ def main():
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
                 if k in m:
                     rec[k.lower()[3:] + "_frac"] = round(m[k] / m["SQ_WAVE_CYCLES"], 4)
-        if "SQ_INSTS_MFMA" in m:
+        if m.get("SQ_INSTS_MFMA", 0) > 0:
             for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
                 if k in m:
                     rec[k.lower()[9:] + "_per_mfma"] = round(m[k] / m["SQ_INSTS_MFMA"], 3)
@@ -72,7 +72,7 @@ def main():
         if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
             rec["l2_hit"] = round(m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 4)
         if "SQ_LDS_IDX_ACTIVE" in m:
-            rec["lds_active_per_mfma"] = round(m["SQ_LDS_IDX_ACTIVE"] / m.get("SQ_INSTS_MFMA", 1), 3)
+            rec["lds_active_per_mfma"] = round(m["SQ_LDS_IDX_ACTIVE"] / max(1.0, m.get("SQ_INSTS_MFMA", 1)), 3)
         out[f"{key[0]} grid {key[1]}"] = rec
     print(json.dumps(out, indent=1))
 
