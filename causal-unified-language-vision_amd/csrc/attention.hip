@@ -105,8 +105,12 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // box, profiles/r04/attn/attn_fwd_ab.txt)
 int g_fwd_stage = -1;
 // backward staging (cullavo_attn_set_bwd_stage): bit 0 = dK/dV Q / dO by LDS-DMA, bit 1 = the
-// dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT)
-int g_bwd_stage = 0;
+// dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT). Round 5: with bit 0 the
+// dK/dV kernel reads every fragment by inline asm one step ahead of its MFMAs (no vmcnt(0) in
+// front of the reads, the dS^T stores left in flight at the tile's end): 7B layer backward
+// 467.5 -> 449.7 us, bitwise equal (profiles/r05/attn/attn_bwd_stage_ab.txt), so bit 0 is the
+// default
+int g_bwd_stage = 1;
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
 
@@ -259,6 +263,38 @@ struct StageDMA1 {
 
 // row of accumulator register r of a 32x32 tile for lane half h
 DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// a transposed fragment from its two ds_read_b64_tr_b16 halves
+DEV frag8 tr_join(const s16x4& lo, const s16x4& hi) {
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(frag8, v);
+}
+
+// four row fragments by inline-asm ds_read_b128 / four transposed halves by ds_read_b64_tr_b16
+// (issued together), and the counted lgkmcnt wait that ties a group's registers before use
+DEV void rd4(s16x8& a, s16x8& b, s16x8& c, s16x8& d, unsigned pa, unsigned pb, unsigned pc, unsigned pd) {
+  asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7"
+               : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+               : "v"(pa), "v"(pb), "v"(pc), "v"(pd)
+               : "memory");
+}
+template <int CNT>
+DEV void tie4(s16x8& a, s16x8& b, s16x8& c, s16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+DEV void rd4t(s16x4& a, s16x4& b, s16x4& c, s16x4& d, unsigned pa, unsigned pb, unsigned pc, unsigned pd) {
+  asm volatile("ds_read_b64_tr_b16 %0, %4\n\tds_read_b64_tr_b16 %1, %5\n\tds_read_b64_tr_b16 %2, %6\n\t"
+               "ds_read_b64_tr_b16 %3, %7"
+               : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+               : "v"(pa), "v"(pb), "v"(pc), "v"(pd)
+               : "memory");
+}
+template <int CNT>
+DEV void tie4t(s16x4& a, s16x4& b, s16x4& c, s16x4& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(CNT) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 // Forward STAGE 5: the P V^T product's V^T fragments through inline-asm ds_read_b64_tr_b16 (one
 // group = the ND fragments of one 16-key slice, VB the slice's LDS byte offset as an immediate),
@@ -1470,9 +1506,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
   // DMA (cullavo_attn_set_bwd_stage(1)): Q / dO tiles by LDS-DMA into the swizzled image (as the
   // forward's StageDMA), no staging registers or ds_write
   StageDMA<QT, D, 8> dq_, ddo_;
+  // DMA: per-lane LDS byte offsets of the asm fragment reads (rows relative to a 32-row slice /
+  // a 16-key slice: the image swizzle depends on row & 15 only)
+  unsigned roff_b[NS], toff_b[ND][2];
   if constexpr (DMA) {
     dq_.prep(ldq, wave, lane);
     ddo_.prep(lddo, wave, lane);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) roff_b[s] = kv_off<D>(lane & 31, 2 * s + (lane >> 5));
+    const int i = lane & 15, qq = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int ch = ((dt * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (pp >> 1);
+      toff_b[dt][0] = kv_off<D>(4 * hf + qq, ch) + 8 * (pp & 1);
+      toff_b[dt][1] = kv_off<D>(4 * hf + qq + 8, ch) + 8 * (pp & 1);
+    }
   }
   float aux = 0.f;
   // the next tile's lse / delta: loaded raw and first used when staged after the tile's compute
@@ -1533,10 +1581,36 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     const float* sdel = slse + QT;
     // S[q][key], dP[q][key] for this wave's 32 query rows of the tile
     f32x16 sacc = f32x16(0.f), pacc = f32x16(0.f);
+    if constexpr (DMA) {
+      // inline-asm fragment reads (a compiler-visible LDS read may alias the next tile's in-flight
+      // LDS-DMA, so hipcc would wait vmcnt(0) in front of it), one k-step ahead of the MFMAs: the
+      // four reads of step s + 1 are in flight while step s's two MFMAs issue
+      const unsigned aq = lds_addr(buf) + 2u * D * 32u * u, ak = lds_addr(sK) + 2u * D * 32u * ksl;
+      s16x8 q0, k0, d0, v0, q1, k1, d1, v1;
+      __builtin_amdgcn_sched_barrier(0);
+      rd4(q0, k0, d0, v0, aq + roff_b[0], ak + roff_b[0], aq + TQ + roff_b[0], ak + TK + roff_b[0]);
+#pragma unroll
+      for (int st = 0; st < NS; st += 2) {
+        rd4(q1, k1, d1, v1, aq + roff_b[st + 1], ak + roff_b[st + 1], aq + TQ + roff_b[st + 1], ak + TK + roff_b[st + 1]);
+        tie4<4>(q0, k0, d0, v0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, q0), __builtin_bit_cast(frag8, k0), sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, d0), __builtin_bit_cast(frag8, v0), pacc, 0, 0, 0);
+        if (st + 2 < NS) {
+          rd4(q0, k0, d0, v0, aq + roff_b[st + 2], ak + roff_b[st + 2], aq + TQ + roff_b[st + 2], ak + TK + roff_b[st + 2]);
+          tie4<4>(q1, k1, d1, v1);
+        } else {
+          tie4<0>(q1, k1, d1, v1);
+        }
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, q1), __builtin_bit_cast(frag8, k1), sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(frag8, d1), __builtin_bit_cast(frag8, v1), pacc, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf, 32 * u, s, lane), row_frag<D>(sK, 32 * ksl, s, lane), sacc, 0, 0, 0);
       pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<D>(buf + TQ, 32 * u, s, lane), row_frag<D>(sV, 32 * ksl, s, lane), pacc, 0, 0, 0);
+    }
     }
     // query qq is live for this lane's key iff qlo <= qq < qlim: one unsigned compare per element
     const int qoff = qt * QT + 32 * u + 4 * hf - qlo;
@@ -1566,10 +1640,36 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
         *reinterpret_cast<u16x4*>(row) = u16x4{w[0], w[1], w[2], w[3]};
         *reinterpret_cast<u16x4*>(row + 8) = u16x4{w[4], w[5], w[6], w[7]};
       }
+      if constexpr (DMA) {
+        // transposed dO / Q fragments by inline asm, one column block ahead of the MFMAs
+        const unsigned kb = lds_addr(buf) + 2u * D * (32u * u + 16u * s);
+        s16x4 dl0, dh0, ql0, qh0, dl1, dh1, ql1, qh1;
+        __builtin_amdgcn_sched_barrier(0);
+        rd4t(dl0, dh0, ql0, qh0, kb + TQ + toff_b[0][0], kb + TQ + toff_b[0][1], kb + toff_b[0][0], kb + toff_b[0][1]);
+#pragma unroll
+        for (int dt = 0; dt < ND; dt += 2) {
+          rd4t(dl1, dh1, ql1, qh1, kb + TQ + toff_b[dt + 1][0], kb + TQ + toff_b[dt + 1][1], kb + toff_b[dt + 1][0],
+               kb + toff_b[dt + 1][1]);
+          tie4t<4>(dl0, dh0, ql0, qh0);
+          dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_join(dl0, dh0), dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_join(ql0, qh0), dk[dt], 0, 0, 0);
+          if (dt + 2 < ND) {
+            rd4t(dl0, dh0, ql0, qh0, kb + TQ + toff_b[dt + 2][0], kb + TQ + toff_b[dt + 2][1], kb + toff_b[dt + 2][0],
+                 kb + toff_b[dt + 2][1]);
+            tie4t<4>(dl1, dh1, ql1, qh1);
+          } else {
+            tie4t<0>(dl1, dh1, ql1, qh1);
+          }
+          dv[dt + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_join(dl1, dh1), dv[dt + 1], 0, 0, 0);
+          dk[dt + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_join(ql1, qh1), dk[dt + 1], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt) {
         dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, tr_frag<D>(buf + TQ, 32 * u + 16 * s, dt * 32, lane), dv[dt], 0, 0, 0);
         dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(df, tr_frag<D>(buf, 32 * u + 16 * s, dt * 32, lane), dk[dt], 0, 0, 0);
+      }
       }
     }
     if (more) {
@@ -1581,7 +1681,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     }
     if constexpr (DMA) {  // the next tile's DMA landed (MFMAs kept in front of the wait)
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // DS_OUT: the tile's four dS^T stores (two 8-B stores per 16-query slice, after the DMA in
+      // issue order) may stay in flight
+      if constexpr (DS_OUT) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
   }

@@ -309,8 +309,9 @@ int cullavo_attn_set_bwd_tiles(int mode);
 int cullavo_attn_set_stage(int buffer_loads);
 /* A/B switch for the backward's tile staging, two bits: bit 0 = the 8-wave dK/dV kernel's
    (modes 4, 5, 7) Q / dO tiles, bit 1 = the mode-7 dQ kernel's K / dS^T tiles by LDS-DMA
-   straight into the swizzled image (else through registers and ds_write; 0 = the default).
-   Results are identical. Other values leave the setting; returns the previous one. */
+   straight into the swizzled image (else through registers and ds_write); the default is 1
+   (round 5: with LDS-DMA staging the dK/dV kernel's fragment reads are inline asm, one step ahead
+   of the MFMAs). Results are identical. Other values leave the setting; returns the previous one. */
 int cullavo_attn_set_bwd_stage(int mode);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
    move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in
