@@ -1,6 +1,6 @@
 """Static check of the built library's machine code (no GPU): the kernels that issue LDS reads as
 inline asm and wait for them later with a counted `s_waitcnt lgkmcnt(N)` (attention forward stages
-5 / 7) are only
+5 / 7, the LDS-DMA dK/dV backward kernel) are only
 correct if nothing reads or overwrites a read's destination registers before that wait. The
 compiler does not know the data lands late: a spill store, a register copy or a branch placed
 between the read and its wait would use stale values (round 4: a spill store of in-flight
@@ -19,7 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "causal-unified-language-vision_amd", "libcullavo_hip.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 # kernels whose LDS reads are inline asm with deferred counted waits
-ASM_READ_KERNELS = ("attn_fwd_pipe_k", "attn_fwd_kILi128ELb1ELi5E", "attn_fwd_kILi64ELb0ELi5E")
+ASM_READ_KERNELS = ("attn_fwd_pipe_k", "attn_fwd_kILi128ELb1ELi5E", "attn_fwd_kILi64ELb0ELi5E",
+                    # round 5: the LDS-DMA dK/dV kernel's fragment reads (DMA = true instantiations)
+                    "attn_bwd_dkdv8_kILi128ELb1ELb1ELb1E", "attn_bwd_dkdv8_kILi128ELb1ELb0ELb1E",
+                    "attn_bwd_dkdv8_kILi128ELb0ELb1ELb1E", "attn_bwd_dkdv8_kILi128ELb0ELb0ELb1E",
+                    "attn_bwd_dkdv8_kILi64ELb1ELb1ELb1E", "attn_bwd_dkdv8_kILi64ELb0ELb1ELb1E",
+                    "attn_bwd_dkdv8_kILi64ELb1ELb0ELb1E", "attn_bwd_dkdv8_kILi64ELb0ELb0ELb1E")
 
 
 def _regs(spec):
