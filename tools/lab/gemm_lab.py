@@ -12,7 +12,9 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SHAPES = {"qkv": (8704, 12288, 4096), "o": (8704, 4096, 4096), "gate_up": (8704, 22016, 4096),
-          "down": (8704, 4096, 11008), "lm_head": (8704, 32064, 4096)}
+          "down": (8704, 4096, 11008), "lm_head": (8704, 32064, 4096),
+          "vit_fc1": (36928, 4096, 1024), "vit_qkv": (36928, 3072, 1024), "vit_o": (36928, 1024, 1024),
+          "vit_fc2": (36928, 1024, 4096)}
 
 
 def main():
