@@ -71,7 +71,7 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, c
 // unfused product stores them -- bitwise swiglu_fwd_k of that product, without its launch or the
 // [M, 2N] round trip.
 template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves, int OT = 0>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : NBW >= 8 ? 4 : 8))) void gemv_k(GemvArgs a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : (NBW >= 8 || XF == 1) ? 4 : 8))) void gemv_k(GemvArgs a) {
   static_assert(OT == 0 || RB == 1, "SwiGLU pairing: one 16-row block per workgroup");
   const GemmArgs& p = a.g;
   __shared__ f32x4 red[NW][RB][64];
@@ -99,6 +99,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int NB = NBW / RB;  // k-steps per batch (W loads per batch stay NBW)
+  // XF 1: the first XR 16-B chunks of the raw rows per thread and the norm weight chunk of the first
+  // one, loaded ahead of the weight batch so the normalisation waits on them alone
+  constexpr int XR = XF == 1 ? 2 : 1;
+  __shared__ float xrs[XF == 1 ? 16 : 1];
+  u16x8 xpre[XR], wpre{};
+  int64_t wcol = -1;
+  if constexpr (XF == 1) {
+    const int64_t cpr = p.K / 8, Q = p.M * cpr;
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int64_t q = threadIdx.x + (int64_t)(64 * NW) * i;
+      xpre[i] = u16x8{};
+      if (q < Q) {
+        const int64_t row = q / cpr, col = (q - row * cpr) * 8;
+        xpre[i] = *reinterpret_cast<const u16x8*>(p.A + row * p.lda + col);
+      }
+    }
+    if ((int64_t)threadIdx.x < Q) {
+      wcol = ((int64_t)threadIdx.x % cpr) * 8;
+      wpre = *reinterpret_cast<const u16x8*>(a.xf_w + wcol);
+    }
+  }
   for (int64_t j0 = 0; j0 < per; j0 += NB) {
     frag8 w[NB][RB], x[NB];
 #pragma unroll
@@ -113,54 +135,51 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
         w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
     }
     if (XF == 1 && j0 == 0) {
-      // RMSNorm of the M rows, after the first batch of weight loads is in flight: rmsnorm_fwd_k's
-      // arithmetic (one wave per row, the same summation order, y = w * rnd(x * rstd)) written
-      // once into LDS, handed over with a barrier that waits on the LDS only (the weight loads stay
-      // in flight); every later x fragment is an LDS read
+      // RMSNorm of the M rows, after the first batch of weight loads is in flight, by every thread of
+      // the workgroup (round 4/5 ran one wave per row through 8 dependent load rounds: ~10 us per
+      // launch): (1) the raw rows into LDS (the first XR chunks per thread were loaded before the
+      // weight batch), (2) wave w < M sums row w's squares in rmsnorm_fwd_k's order (lane: chunks c,
+      // then elements j; norms.hip) from LDS, (3) every thread normalises its chunks in place,
+      // y = bf16(w * bf16(x * rstd)). Barriers wait on the LDS only (the weight loads stay in flight).
+      const int64_t cpr = p.K / 8, Q = p.M * cpr;
+#pragma unroll
+      for (int i = 0; i < XR; ++i) {
+        const int64_t q = threadIdx.x + (int64_t)(64 * NW) * i;
+        if (q < Q) {
+          const int64_t row = q / cpr, col = (q - row * cpr) * 8;
+          *reinterpret_cast<u16x8*>(xs + row * xs_ld + col) = xpre[i];
+        }
+      }
+      for (int64_t q = threadIdx.x + (int64_t)(64 * NW) * XR; q < Q; q += 64 * NW) {
+        const int64_t row = q / cpr, col = (q - row * cpr) * 8;
+        *reinterpret_cast<u16x8*>(xs + row * xs_ld + col) = *reinterpret_cast<const u16x8*>(p.A + row * p.lda + col);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
       for (int row = wave; row < p.M; row += NW) {
-        const u16* xr = p.A + row * p.lda;
         float ss = 0.f;
-        // 2 row loads in flight per round (more spilled the 4- and 8-load variants, whose
-        // waves_per_eu caps them at 64 / 128 registers: the round-4 form with 8 in flight ran the
-        // products 2-3x slower out of scratch); the accumulation order (chunk, then element) is
-        // rmsnorm_fwd_k's whatever the batching
-        for (int c0 = 0; c0 * 512 < p.K; c0 += 2) {
-          u16x8 xv[2];
+        for (int c = 0; c * 512 < p.K; ++c) {
+          const int col = c * 512 + lane * 8;
+          if (col < p.K) {
+            const u16x8 xv = *reinterpret_cast<const u16x8*>(xs + row * xs_ld + col);
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = (c0 + c) * 512 + lane * 8;
-            xv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(xr + col) : u16x8{};
-          }
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = (c0 + c) * 512 + lane * 8;
-            if (col < p.K) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) ss += bf2f(xv[c][j]) * bf2f(xv[c][j]);
-            }
+            for (int j = 0; j < 8; ++j) ss += bf2f(xv[j]) * bf2f(xv[j]);
           }
         }
         ss = wave_sum(ss);
-        const float rr = rsqrtf(ss / (float)p.K + a.xf_eps);
-        for (int c0 = 0; c0 * 512 < p.K; c0 += 2) {
-          u16x8 xv[2], wv[2];
+        if (lane == 0) xrs[row] = rsqrtf(ss / (float)p.K + a.xf_eps);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      for (int64_t q = threadIdx.x; q < Q; q += 64 * NW) {
+        const int64_t row = q / cpr, col = (q - row * cpr) * 8;
+        const u16x8 wv = col == wcol ? wpre : *reinterpret_cast<const u16x8*>(a.xf_w + col);
+        const u16x8 xv = *reinterpret_cast<const u16x8*>(xs + row * xs_ld + col);
+        const float rr = xrs[row];
+        u16x8 o;
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = (c0 + c) * 512 + lane * 8;
-            xv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(xr + col) : u16x8{};
-            wv[c] = col < p.K ? *reinterpret_cast<const u16x8*>(a.xf_w + col) : u16x8{};
-          }
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = (c0 + c) * 512 + lane * 8;
-            if (col < p.K) {
-              u16x8 o;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wv[c][j]) * round_bf(bf2f(xv[c][j]) * rr));
-              *reinterpret_cast<u16x8*>(xs + row * xs_ld + col) = o;
-            }
-          }
-        }
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wv[j]) * round_bf(bf2f(xv[j]) * rr));
+        *reinterpret_cast<u16x8*>(xs + row * xs_ld + col) = o;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

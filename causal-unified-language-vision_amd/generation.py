@@ -31,8 +31,12 @@ import os
 #           transform 3: one launch instead of the product + cullavo_swiglu_fwd);
 #   "rope"  (default on) RoPE + KV append inside decode attention (cullavo_attn_decode_rope);
 #   "norm"  the two RMSNorms into the q|k|v and gate|up products' X loads, "swiglu" the SwiGLU into
-#           down_proj's X loads (measured ~2x slower per product, profiles/r04/decode/decode_fusions_ab.txt:
-#           off by default)
+#           down_proj's X loads (round 4: ~2x slower per product, profiles/r04/decode/decode_fusions_ab.txt;
+#           round 5, the whole workgroup normalising: 3.73 vs 3.53 ms per token at batch 1, 4.67 vs
+#           4.02 at batch 4 -- every workgroup redoing the row norm still costs more than the one
+#           norm launch: off by default). A norm in the TAIL of o_proj / down_proj instead (the last
+#           workgroup by an agent-scope counter normalises the rows) measured 3.78 vs 3.53 ms
+#           (profiles/r05/decode/pnorm_ab_*): not kept
 _FUSE = {f.strip() for f in os.environ.get("CULLAVO_DECODE_FUSE", "gu,rope").split(",") if f.strip()}
 FUSE_DECODE_NORMS = "norm" in _FUSE
 FUSE_DECODE_SWIGLU = "swiglu" in _FUSE
