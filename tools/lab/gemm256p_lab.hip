@@ -10,9 +10,10 @@
 //   VAR bit 2: full __syncthreads in the epilogue (the production epilogue's waits)
 //   VAR bit 3: ablation: no global stores (the epilogue's LDS round trip and conversion stay)
 //   VAR bit 4: ablation: no epilogue at all
+//   VAR bits 7/8: the same stagger within each XCD (odd CUs of every XCD late)
 //   VAR bits 5/6: stagger -- the blocks of XCDs 4-7 start ~8 us (bit 5) / ~16 us (bit 6) late, so the two
 //              XCD halves store their epilogues at different times (each XCD keeps its own lock-step)
-// Layout (0,0) and (1,1), bf16 out; for tools/lab/gemm_lab.py (v = 300 + VAR: persistent; 400 + VAR: (1,1)).
+// Layout (0,0) and (1,1), bf16 out; for tools/lab/gemm_lab.py (v = 1000 + VAR: persistent, layout (0,0)).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC tools/lab/gemm256p_lab.hip \
 //     -o tools/lab/bin/libgemm256p_lab.so
 #include "../../causal-unified-language-vision_amd/csrc/gemm_common.h"
@@ -105,6 +106,10 @@ __global__ __launch_bounds__(512, 1) void gemm256p_k(GemmArgs p) {
   if (t >= tiles) return;
   if ((VAR & 96) && (blockIdx.x & 7) >= 4) {
     const int n = (VAR & 32 ? 2 : 0) + (VAR & 64 ? 4 : 0);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  if ((VAR & 384) && ((blockIdx.x >> 3) & 1)) {  // within-XCD stagger: every other CU of each XCD late
+    const int n = (VAR & 128 ? 2 : 0) + (VAR & 256 ? 4 : 0);
     for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
   }
 
@@ -211,12 +216,9 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
   p.M = M; p.N = N; p.K = K; p.lda = K; p.ldb = K; p.ldc = N;
   p.alpha = 1.f; p.act = CULLAVO_ACT_NONE; p.epi_lds = 1; p.group_m = -4; p.dma_pre = 1;
   hipStream_t s = (hipStream_t)stream;
-  if (v >= 400) {  // layout (1,1): A^T stored [K][M], B^T stored [K][N] (the dW product's layouts)
-    p.lda = M; p.ldb = N;
-  }
   switch (v) {
-#define C(V) case 300 + V: return launch_p<0, 0, V>(p, s); case 400 + V: return launch_p<1, 1, V>(p, s);
-    C(0) C(2) C(8) C(32) C(64) C(96) C(34) C(66)
+#define C(V) case 1000 + V: return launch_p<0, 0, V>(p, s);
+    C(0) C(2) C(8) C(128) C(256) C(130) C(258)
 #undef C
   }
   return 2;
