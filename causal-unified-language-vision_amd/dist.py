@@ -190,9 +190,6 @@ class GradReducer:
             b["pending"].clear()
         self._issue_ready()
         assert self._next == len(self.buckets)
-        t0 = time.perf_counter()
-        self._finish_agree_skipped(pending)
-        host_ms = (time.perf_counter() - t0) * 1e3
         scale = 1.0 / self.world
 
         def _complete():
@@ -201,6 +198,9 @@ class GradReducer:
                 if not self.avg_supported:
                     self.arenas[b["arena"]].grad_flat[b["lo"]:b["hi"]].mul_(scale)
 
+        # every bucket's completion is queued on the GPU before the host waits for the written-key
+        # agreement (needed only by the optimizer step that follows: which keys move)
+        ev_done = None
         if self.stream is not None:
             with torch.cuda.stream(self.stream):
                 _complete()
@@ -208,9 +208,13 @@ class GradReducer:
             if ev_bwd is not None:
                 ev_done = torch.cuda.Event(enable_timing=True)
                 ev_done.record(cur)
-                self.exposure.append((ev_bwd, ev_done, host_ms))
         else:
             _complete()
+        t0 = time.perf_counter()
+        self._finish_agree_skipped(pending)
+        host_ms = (time.perf_counter() - t0) * 1e3
+        if ev_done is not None:
+            self.exposure.append((ev_bwd, ev_done, host_ms))
         self.reset()
 
     def exposure_stats(self) -> dict | None:
