@@ -21,6 +21,7 @@ _CTYPE = {
     "float": ctypes.c_float,
     "double": ctypes.c_double,
     "size_t": ctypes.c_size_t,
+    "uint64_t": ctypes.c_uint64,
 }
 
 DT_F32 = 0

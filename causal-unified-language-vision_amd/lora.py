@@ -28,12 +28,16 @@ forward and both backward uses regenerate it instead of storing it.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
 
 from . import ops
 from .ops import DROP_A, DROP_B, DROP_OUT
+
+# CULLAVO_LORA_DX_FUSE=0: the per-module dx products instead of cullavo_lora_dx (A/B switch)
+LORA_DX_FUSE = os.environ.get("CULLAVO_LORA_DX_FUSE", "1") != "0"
 
 LM_TARGETS = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
 VISION_TARGETS = ("q_proj", "k_proj", "v_proj", "fc1", "fc2")
@@ -221,14 +225,20 @@ class LoraGroup:
                         alpha=self.scaling, beta=beta)
         if self.dropping(train):
             p = self.s.lora_dropout
+            seeds = [module_seed(step_seed, self.uid, m) for m in range(self.n)]
+            # the group's dx contributions in one pass over dx (cullavo_lora_dx, bitwise the
+            # per-module products below)
+            fused_dx = (LORA_DX_FUSE and dx is not None and dx.dtype == torch.bfloat16 and r == 64
+                        and self.n <= 3)
             for m in range(self.n):
-                seed = module_seed(step_seed, self.uid, m)
                 g, beta = ar.grad_slot(self.a_keys[m])
                 ops.gemm_ex(1, 1, r, self.in_f, M, du[:, m * r:], R, x, ldx, g, self.in_f, beta=beta,
-                            drop_operand=DROP_B, drop_p=p, drop_seed=seed)
-                if dx is not None:
+                            drop_operand=DROP_B, drop_p=p, drop_seed=seeds[m])
+                if dx is not None and not fused_dx:
                     ops.gemm_ex(0, 1, M, self.in_f, r, du[:, m * r:], R, self.A(m), self.in_f, dx, ops._ld(dx),
-                                beta=1.0, drop_operand=DROP_OUT, drop_p=p, drop_seed=seed)
+                                beta=1.0, drop_operand=DROP_OUT, drop_p=p, drop_seed=seeds[m])
+            if fused_dx:
+                ops.lora_dx(du, self.a_stack(), dx, n_mod=self.n, drop_p=p, seeds=seeds)
         else:
             g, beta = ar.grad_slot(self.a_keys[0], (R, self.in_f))
             ar.mark_written(self.a_keys[1:])

@@ -343,6 +343,18 @@ def swiglu_fwd(gu):
     return out
 
 
+def lora_dx(du, a_stack, dx, *, n_mod: int, drop_p: float, seeds):
+    """dx += the LoRA group's input gradient through its dropout, one launch (cullavo_lora_dx):
+    for m in order, dx = bf16(dx + mask_m / (1-p) * du[:, 64m:64m+64] @ a_stack[64m:64m+64]),
+    bitwise the per-module gemm_ex(0, 1, ..., drop_operand=DROP_OUT, beta=1) calls."""
+    _dev(du, a_stack, dx)
+    M, N = dx.shape
+    s = [int(x) for x in seeds] + [0] * (3 - len(seeds))
+    call("lora_dx", int(n_mod), M, N, _ptr(du), _ld(du), _ptr(a_stack), _ld(a_stack), _ptr(dx), _ld(dx),
+         float(drop_p), s[0], s[1], s[2], _stream())
+    return dx
+
+
 def decode_linear(x, w, *, transform: int = 0, norm_w=None, eps: float = 0.0, residual=None):
     """Decode rows (M <= 16) through cullavo_decode_linear: y = T(x) @ w.T (+ residual) with T the
     fused input transform (0 none, 1 RMSNorm with norm_w / eps, 2 SwiGLU of x = gate|up [M, 2K]);

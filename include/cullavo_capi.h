@@ -139,6 +139,18 @@ size_t cullavo_gemm_desc_size(void);
 /* bytes of split-K workspace cullavo_gemm_ex would use for this problem (0: no split) */
 size_t cullavo_gemm_workspace(const cullavo_gemm_desc* desc);
 
+/* LoRA adapters' input gradient through their dropout, one launch per adapter group (peft
+ * LoraLayer backward, reference cullavo/load_cullavo.py:94-112):
+ *   for m = 0 .. n_mod-1 in order: dx = bf16(dx + mask_m / (1 - drop_p) * (du_m A_m))
+ * du [M, ld_du] bf16 holds module m's du in columns m*64 .. m*64+63; a_stack [n_mod*64, ld_a] bf16
+ * holds lora_A.weight of module m in rows m*64 ..; dx [M, ld_dx] bf16 is accumulated in place;
+ * mask_m is the dropout hash of seed_m (csrc/common.h drop_keep, as cullavo_gemm_ex's
+ * drop_operand 3). Bitwise the n_mod per-module cullavo_gemm_ex launches (layouts (0,1), K = 64,
+ * drop_operand 3, beta 1) it replaces, in one pass over dx. 1 <= n_mod <= 3, N % 8 == 0. */
+int cullavo_lora_dx(int n_mod, int64_t M, int64_t N, const void* du, int64_t ld_du, const void* a_stack,
+                    int64_t ld_a, void* dx, int64_t ld_dx, float drop_p, uint64_t seed0, uint64_t seed1,
+                    uint64_t seed2, void* stream);
+
 /* Kernel-shape selection for cullavo_gemm: -1 = automatic (default), 0 = 128x128 tile /
  * 4 waves (register staged), 2 = 256x256 / 8 waves, 3 = 192x256 / 8 waves, 10 = 288x256 / 8 waves
  * (LDS-DMA staged; 3 and 10 fall back to 2 when A is not K-contiguous; 10 is chosen automatically

@@ -137,6 +137,36 @@ def test_gemm_dropout_operands_and_output():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_mod,M,N,p", [(3, 8704, 4096, 0.05), (2, 1031, 4096, 0.05), (1, 8704, 4096, 0.05),
+                                         (3, 1154, 1024, 0.3), (2, 300, 264, 0.05), (1, 36928, 1024, 0.05)])
+def test_lora_dx_group_bitwise(n_mod, M, N, p):
+    """cullavo_lora_dx (the adapter group's dropout-masked dx contributions in one pass over dx) is
+    bitwise the per-module gemm_ex(0, 1, K = 64, drop_operand 3, beta 1) launches it replaces, and
+    matches mask * (du A) / (1 - p) in fp32 (the mask from the oracle's hash restatement)."""
+    from cullavo_amd import ops
+    from cullavo_amd.lora import module_seed
+    g = torch.Generator().manual_seed(n_mod * 1000 + M + N)
+    du = (torch.randn(M, 64 * n_mod, generator=g) * 0.1).to(BF).cuda()
+    A = (torch.randn(64 * n_mod, N, generator=g) * 0.05).to(BF).cuda()
+    dx0 = torch.randn(M, N, generator=g).to(BF).cuda()
+    seeds = [module_seed(12345, 7, m) for m in range(n_mod)]
+    ref = dx0.clone()
+    for m in range(n_mod):
+        ops.gemm_ex(0, 1, M, N, 64, du[:, 64 * m:], 64 * n_mod, A[64 * m:], N, ref, N, beta=1.0,
+                    drop_operand=ops.DROP_OUT, drop_p=p, drop_seed=seeds[m])
+    got = dx0.clone()
+    ops.lora_dx(du, A, got, n_mod=n_mod, drop_p=p, seeds=seeds)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    if M * N <= 4096 * 1200:  # fp32 restatement with the oracle's mask on the smaller cases
+        want = dx0.float().cpu()
+        for m in range(n_mod):
+            keep = torch.from_numpy(O.lora_keep_mask(seeds[m], M, N, p)).float()
+            want = want + keep * (du[:, 64 * m:64 * m + 64].float().cpu() @ A[64 * m:64 * m + 64].float().cpu()) / (1 - p)
+        close(got, want, 1e-2, "lora dx")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,al,bl", [(64, 4096, 8704, 1, 1), (8704, 64, 4096, 0, 0), (8704, 64, 11008, 0, 1),
                                          (4096, 64, 8704, 1, 1), (200, 136, 3000, 0, 0)])
 def test_gemm_split_k(M, N, K, al, bl):
