@@ -102,6 +102,8 @@ def lib():
             L.cullavo_gemm_set_msplit(int(os.environ["CULLAVO_GEMM_MSPLIT"]))
         if os.environ.get("CULLAVO_GEMM_GROUP"):  # tile-order A/B (cullavo_gemm_set_group)
             L.cullavo_gemm_set_group(int(os.environ["CULLAVO_GEMM_GROUP"]))
+        if os.environ.get("CULLAVO_GEMM_EPILOGUE"):  # epilogue A/B: bit 0 LDS-staged, bit 1 nt stores
+            L.cullavo_gemm_set_epilogue(int(os.environ["CULLAVO_GEMM_EPILOGUE"]))
         if os.environ.get("CULLAVO_GEMM_DMA"):  # DMA-offset A/B (cullavo_gemm_set_dma)
             L.cullavo_gemm_set_dma(int(os.environ["CULLAVO_GEMM_DMA"]))
         if os.environ.get("CULLAVO_RATE288") is not None:  # 288-row tile A/B (0 = out of the plan)

@@ -379,11 +379,38 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
 // 8 contiguous columns each, so every global access is a full-width 16-B access and 32 lanes
 // cover one 512-B output row (the per-lane 8-B stores of the MFMA layout touch 16 rows per
 // instruction; measured +3-4 % on the whole GEMM, tools/lab/gemm_lab.hip).
+// item i of a half's LDS image: 8 consecutive f32 outputs of one row (thread idx = tid + 512 i:
+// row idx >> 5, columns (idx & 31) * 8 ..), and their coordinates
+template <int R>
+DEV void lds_epi_item(const char* smem, int i, int half, int64_t m0, int64_t n0, float (&v)[8], int64_t& m,
+                      int64_t& n) {
+  const int idx = threadIdx.x + 512 * i;
+  const int r = idx >> 5, pr = idx & 31;
+  const int sw = (pr >> 3) & 1;  // odd chunk first for pairs 8-15, 24-31: conflict-free reads
+  const int c0 = 2 * pr + sw, c1 = 2 * pr + 1 - sw;
+  const char* rowp = smem + r * 1024;
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(rowp + ((c0 ^ (r & 15)) << 4));
+  const f32x4 x1 = *reinterpret_cast<const f32x4*>(rowp + ((c1 ^ (r & 15)) << 4));
+  const f32x4 lo = sw ? x1 : x0, hi = sw ? x0 : x1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+  m = m0 + half * R + r;
+  n = n0 + pr * 8;
+}
+
 template <int CT, int BM2, int TMW, int TN>
 DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wm,
                       int wn, int lane) {
   static_assert(TN == 4, "256-column tiles");
   constexpr int R = BM2 / 2;
+  // plain bf16 outputs (no bias / addend / activation / residual / beta / output dropout / nt: the
+  // q|k|v, gate|up and lm_head products, every dX without a residual and every dW): store8's
+  // arithmetic reduces to o = bf16(alpha * acc), written by a lean loop. The general store8 path
+  // (runtime-checked epilogue options per 8 columns) measured ~1/4 of a K = 1024 product and ~1/10
+  // of a K = 4096 one (tools/lab/gemm256p_lab.hip, profiles/r05/gemm/persistent_lab.txt).
+  const bool plain = CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_NONE && p.preact == nullptr && p.bias == nullptr &&
+                     p.addend == nullptr && p.residual == nullptr && p.beta == 0.f && p.drop_mode != 3 &&
+                     !p.nt_store;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if (wm == half) {
@@ -397,20 +424,27 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
         }
     }
     __syncthreads();
+    if (plain) {  // two versions of the loop, chosen once (uniform)
 #pragma unroll
-    for (int i = 0; i < R * 32 / 512; ++i) {
-      const int idx = threadIdx.x + 512 * i;
-      const int r = idx >> 5, pr = idx & 31;
-      const int sw = (pr >> 3) & 1;  // odd chunk first for pairs 8-15, 24-31: conflict-free reads
-      const int c0 = 2 * pr + sw, c1 = 2 * pr + 1 - sw;
-      const char* rowp = smem + r * 1024;
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(rowp + ((c0 ^ (r & 15)) << 4));
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(rowp + ((c1 ^ (r & 15)) << 4));
-      const f32x4 lo = sw ? x1 : x0, hi = sw ? x0 : x1;
-      float v[8];
+      for (int i = 0; i < R * 32 / 512; ++i) {
+        float v[8];
+        int64_t m, n;
+        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
+        if (m < p.M && n < p.N) {
+          u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-      store8<CT>(p, v, m0 + half * R + r, n0 + pr * 8);
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] * p.alpha);
+          *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
+        }
+      }
+    } else {  // rolled: one copy of the general store8 per half keeps the kernel's code small
+#pragma unroll 1
+      for (int i = 0; i < R * 32 / 512; ++i) {
+        float v[8];
+        int64_t m, n;
+        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
+        store8<CT>(p, v, m, n);
+      }
     }
     __syncthreads();
   }

@@ -5,7 +5,5 @@ OUT=gpurun_out/r05o
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -u tools/lab/gemm_lab.py --lib tools/lab/bin/libgemm256p_lab.so --prod \
-  --variants 1000,1002,1128,1256,1130,1258 --shapes vit_fc1,vit_qkv,gate_up --rounds 3 > $OUT/lab.txt 2>&1
-rc=$?; cat $OUT/lab.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-rc=$?; tail -2 $OUT/smoke.log; exit $rc
+  --variants 1000,1008,1512,2024,3048 --shapes vit_fc1,vit_qkv,gate_up,qkv --rounds 3 > $OUT/lab.txt 2>&1
+rc=$?; cat $OUT/lab.txt; exit $rc

@@ -11,6 +11,7 @@
 //   VAR bit 3: ablation: no global stores (the epilogue's LDS round trip and conversion stay)
 //   VAR bit 4: ablation: no epilogue at all
 //   VAR bits 7/8: the same stagger within each XCD (odd CUs of every XCD late)
+//   VAR bits 9/10/11: the epilogue's bf16 stores with cache policy sc1 / nt / sc0 sc1
 //   VAR bits 5/6: stagger -- the blocks of XCDs 4-7 start ~8 us (bit 5) / ~16 us (bit 6) late, so the two
 //              XCD halves store their epilogues at different times (each XCD keeps its own lock-step)
 // Layout (0,0) and (1,1), bf16 out; for tools/lab/gemm_lab.py (v = 1000 + VAR: persistent, layout (0,0)).
@@ -82,7 +83,20 @@ DEV void epi_pass(const GemmArgs& p, f32x4 (&acc)[P_TMW][P_TN], char* ep, int64_
       float v[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-      if (VAR & 8) {
+      if (VAR & (512 | 1024 | 2048)) {  // cache-policy variants of the plain bf16 store
+        const int64_t mm = m0 + Q * 64 + r, nn = n0 + pr * 8;
+        if (mm < p.M && nn < p.N) {
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+          u16* dst = reinterpret_cast<u16*>(p.C) + mm * p.ldc + nn;
+          typedef __attribute__((ext_vector_type(4))) unsigned u32x4v;
+          const u32x4v d = __builtin_bit_cast(u32x4v, o);
+          if (VAR & 512) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(d) : "memory");
+          else if (VAR & 1024) __builtin_nontemporal_store(d, reinterpret_cast<u32x4v*>(dst));
+          else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(d) : "memory");
+        }
+      } else if (VAR & 8) {
         if (v[0] == 12345.f && v[7] == -1.f) store8<CULLAVO_DT_BF16>(p, v, m0 + Q * 64 + r, n0 + pr * 8);
       } else {
         store8<CULLAVO_DT_BF16>(p, v, m0 + Q * 64 + r, n0 + pr * 8);
@@ -218,7 +232,7 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
   hipStream_t s = (hipStream_t)stream;
   switch (v) {
 #define C(V) case 1000 + V: return launch_p<0, 0, V>(p, s);
-    C(0) C(2) C(8) C(128) C(256) C(130) C(258)
+    C(0) C(8) C(512) C(1024) C(2048)
 #undef C
   }
   return 2;
