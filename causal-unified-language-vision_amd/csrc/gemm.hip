@@ -476,8 +476,8 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = g_epi_lds | (g_nt_store << 1);
-  g_epi_lds = lds_staged & 1;
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 12);
+  g_epi_lds = lds_staged & 13;  // bit 0 LDS-staged; bits 2 / 3 disable its bias-residual / plain paths
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }
@@ -600,7 +600,9 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
   {
     auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
     p.epi_lds = a16(d.C) && a16(d.bias) && a16(d.preact) && a16(residual) && a16(d.addend) &&
-                (d.addend == nullptr || d.ld_addend % 8 == 0) && g_epi_lds;
+                        (d.addend == nullptr || d.ld_addend % 8 == 0) && (g_epi_lds & 1)
+                    ? g_epi_lds
+                    : 0;
   }
   p.nt_store = g_nt_store;
   p.dma_pre = g_dma_pre && (a_layout == 1 || K % BK == 0) && (b_layout == 1 || K % BK == 0);

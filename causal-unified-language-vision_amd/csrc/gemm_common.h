@@ -408,9 +408,13 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
   // arithmetic reduces to o = bf16(alpha * acc), written by a lean loop. The general store8 path
   // (runtime-checked epilogue options per 8 columns) measured ~1/4 of a K = 1024 product and ~1/10
   // of a K = 4096 one (tools/lab/gemm256p_lab.hip, profiles/r05/gemm/persistent_lab.txt).
-  const bool plain = CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_NONE && p.preact == nullptr && p.bias == nullptr &&
-                     p.addend == nullptr && p.residual == nullptr && p.beta == 0.f && p.drop_mode != 3 &&
-                     !p.nt_store;
+  // bias_res: the same with an optional bias and / or residual (the o_proj / down_proj forward,
+  // the ViT's biased products): store8's v = alpha acc + bias, then bf16(bf16(v) + residual)
+  // (epi_lds bits 2 / 3: A/B switches that send these cases to the general path)
+  const bool lean = CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_NONE && p.preact == nullptr &&
+                    p.addend == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store;
+  const bool plain = lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8);
+  const bool bias_res = lean && !plain && !(p.epi_lds & 4);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if (wm == half) {
@@ -434,6 +438,35 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
           u16x8 o;
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j] * p.alpha);
+          *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
+        }
+      }
+    } else if (bias_res) {
+#pragma unroll
+      for (int i = 0; i < R * 32 / 512; ++i) {
+        float v[8];
+        int64_t m, n;
+        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
+        if (m < p.M && n < p.N) {
+          float b[8], rs[8];
+          if (p.bias) {
+            const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = bf2f(bv[j]);
+          }
+          if (p.residual) {
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rs[j] = bf2f(rv[j]);
+          }
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float x = v[j] * p.alpha;
+            if (p.bias) x += b[j];
+            if (p.residual) x = round_bf(x) + rs[j];
+            o[j] = f2bf(x);
+          }
           *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
         }
       }
