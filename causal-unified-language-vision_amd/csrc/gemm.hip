@@ -476,8 +476,9 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 12);
-  g_epi_lds = lds_staged & 13;  // bit 0 LDS-staged; bits 2 / 3 disable its bias-residual / plain paths
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 28);
+  g_epi_lds = lds_staged & 29;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
+                                // activation + SwiGLU-backward paths
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }

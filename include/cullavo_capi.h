@@ -179,9 +179,9 @@ int cullavo_gemm_set_group(int group);
 int cullavo_gemm_set_splitk_target(int blocks);
 /* Tuning/A-B switch. Bit 0: 1 (default) = the 8-wave kernels stage their epilogue through LDS
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
-   Bit 1: C is written with non-temporal (streaming) stores. Bits 2 / 3 (round 5, A/B): send the
-   LDS epilogue's lean bias/residual and plain-output paths to the general per-option path
-   (same values). Returns the previous setting. */
+   Bit 1: C is written with non-temporal (streaming) stores. Bits 2 / 3 / 4 (round 5, A/B): send
+   the LDS epilogue's lean bias/residual, plain-output and activation / SwiGLU-backward paths to
+   the general per-option path (same values). Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets
    computed once per tile and the K advance passed as the scalar offset (used when K % 64 == 0
