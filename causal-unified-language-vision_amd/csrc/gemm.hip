@@ -256,6 +256,174 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
 
 
 
+int num_cus();
+// ---- persistent 256x256 forward kernel (round 5) ---------------------------------------------
+// Layout (0,0), bf16 C, no split-K / LoRA: one 512-thread block per CU walks the tiles of the grid in
+// the data-parallel kernel's lock-step round order (tile t, t + gridDim, ...; the same XCD remap and
+// group order), the same LDS-DMA K-loop (waves 0-3 load), the next tile's first K-tile issued under
+// the current tile's last MFMAs, and the LDS epilogue in four 64-row passes through the stage the
+// last K-tile freed (64 KiB), each 8-column group written by lds_store_item (the lean paths of
+// lds_epilogue and store8 otherwise: the same values as gemm256_k). Lab record:
+// tools/lab/gemm256p_lab.hip, profiles/r05/gemm/persistent_lab.txt and epilogue/.
+struct PTile { int tm, tn; };
+DEV PTile ptile(const GemmArgs& p, int lid) {  // tile_origin's order by value selects
+  const bool by_n = p.group_m < 0;
+  const int g = by_n ? -p.group_m : p.group_m;
+  const int major = by_n ? p.tiles_n : p.tiles_m;
+  const int minor = by_n ? p.tiles_m : p.tiles_n;
+  const int per_group = g * minor;
+  const int group = lid / per_group;
+  const int first = group * g;
+  const int gsize = min(major - first, g);
+  const int in = lid - group * per_group;
+  const int a = first + in % gsize, b = in / gsize;
+  return by_n ? PTile{b, a} : PTile{a, b};
+}
+
+DEV void praw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+constexpr int P_TA = 256 * BK * 2, P_STAGE = 2 * P_TA;  // 32 KiB A + 32 KiB B per stage
+
+template <int Q, int MODE>
+DEV void p_epi_pass(const GemmArgs& p, f32x4 (&acc)[8][4], char* ep, int64_t m0, int64_t n0, int wm, int wn, int el) {
+  const int elane = el & 63;
+  if (wm == (Q >> 1)) {
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        const int r = t4 * 16 + (elane & 15);
+        const int c = wn * 16 + tn * 4 + (elane >> 4);
+        *reinterpret_cast<f32x4*>(ep + r * 1024 + ((c ^ (r & 15)) << 4)) = acc[(Q & 1) * 4 + t4][tn];
+      }
+  }
+  praw_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = el + 512 * i;
+    const int r = idx >> 5, pr = idx & 31;
+    const int sw = (pr >> 3) & 1;
+    const int c0 = 2 * pr + sw, c1 = 2 * pr + 1 - sw;
+    const char* rowp = ep + r * 1024;
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(rowp + ((c0 ^ (r & 15)) << 4));
+    const f32x4 x1 = *reinterpret_cast<const f32x4*>(rowp + ((c1 ^ (r & 15)) << 4));
+    const f32x4 lo = sw ? x1 : x0, hi = sw ? x0 : x1;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+    lds_store_item<CULLAVO_DT_BF16>(p, v, m0 + Q * 64 + r, n0 + pr * 8, MODE);
+  }
+  praw_barrier();
+}
+
+// MODE: lds_epi_mode's case, fixed per instantiation (a runtime mode per 8-column group kept every
+// path's code in the epilogue and measured slower than the data-parallel kernel)
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void gemm256p_k(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const bool loader = wave < 4;
+  const int lw = wave & 3;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int nk = (int)cdiv(p.K, BK);
+  int t = blockIdx.x;
+  if (t >= tiles) return;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, ((p.M - 1) * p.lda + p.K) * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, ((p.N - 1) * p.ldb + p.K) * 2);
+  PTile xy = ptile(p, xcd_remap(t, p.sk_dp));
+  int64_t m0 = (int64_t)xy.tm * 256, n0 = (int64_t)xy.tn * 256;
+  if (loader) {
+    dma_tile<0, 256, 4>(ra, p.lda, m0, p.M, 0, p.K, smem, lw, lane);
+    dma_tile<0, 256, 4>(rb, p.ldb, n0, p.N, 0, p.K, smem + P_TA, lw, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  praw_barrier();
+  int s = 0;
+  f32x4 acc[8][4];
+  for (;;) {
+    const int t1 = t + (int)gridDim.x;
+    const bool has_next = t1 < tiles;
+    const PTile xy1 = ptile(p, xcd_remap(has_next ? t1 : t, p.sk_dp));
+    const int64_t m1 = (int64_t)xy1.tm * 256, n1 = (int64_t)xy1.tn * 256;
+    unsigned va[dma_per<256, 4>()], vb[dma_per<256, 4>()];
+    dma_prep<0, 256, 4>(p.lda, m0, p.M, lw, lane, va);
+    dma_prep<0, 256, 4>(p.ldb, n0, p.N, lw, lane, vb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = smem + ((s + kt) & 1) * P_STAGE;
+      char* nxt = smem + ((s + kt + 1) & 1) * P_STAGE;
+      if (loader) {
+        if (kt + 1 < nk) {
+          const int64_t k1 = (int64_t)(kt + 1) * BK;
+          dma_issue<256, 4>(ra, va, dma_soff<0>(k1, p.lda), nxt, lw);
+          dma_issue<256, 4>(rb, vb, dma_soff<0>(k1, p.ldb), nxt + P_TA, lw);
+        } else if (has_next) {  // the next tile's first K-tile under this tile's last MFMAs
+          dma_tile<0, 256, 4>(ra, p.lda, m1, p.M, 0, p.K, nxt, lw, lane);
+          dma_tile<0, 256, 4>(rb, p.ldb, n1, p.N, 0, p.K, nxt + P_TA, lw, lane);
+        }
+      }
+      tile_mfma<0, 0, 256, 256, 8, 4>(cur, wm, wn, lane, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      praw_barrier();
+    }
+    char* ep = smem + ((s + nk - 1) & 1) * P_STAGE;  // the last K-tile's stage, free after the barrier
+    // per-lane epilogue indices behind an opaque copy (hoisted out of the tile loop they would stay
+    // live across the K-loop and spill)
+    int el = (int)threadIdx.x;
+    asm volatile("" : "+v"(el));
+    p_epi_pass<0, MODE>(p, acc, ep, m0, n0, wm, wn, el);
+    p_epi_pass<1, MODE>(p, acc, ep, m0, n0, wm, wn, el);
+    p_epi_pass<2, MODE>(p, acc, ep, m0, n0, wm, wn, el);
+    p_epi_pass<3, MODE>(p, acc, ep, m0, n0, wm, wn, el);
+    if (!has_next) break;
+    s = (s + nk) & 1;
+    t = t1;
+    m0 = m1;
+    n0 = n1;
+  }
+}
+
+int g_persist = 1;  // cullavo_gemm_set_epilogue bit 5 turns the persistent forward kernel off (A/B)
+
+template <int MODE>
+int launch256p_m(GemmArgs p, hipStream_t s) {
+  const int smem = 2 * P_STAGE;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm256p_k<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_n = (int)cdiv(p.N, 256);
+  p.sk_dp = p.tiles_m * p.tiles_n;
+  const int grid = std::min(p.sk_dp, num_cus());
+  gemm256p_k<MODE><<<(unsigned)grid, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemm256 persistent");
+}
+
+// the persistent kernel for the lean epilogue cases (plain, bias / residual, activation); -1: none
+int launch256p(const GemmArgs& p, hipStream_t s) {
+  // lds_epi_mode on the host: the same conditions
+  const bool lean = p.act == CULLAVO_ACT_NONE && p.preact == nullptr && p.addend == nullptr && p.beta == 0.f &&
+                    p.drop_mode != 3 && !p.nt_store;
+  if (lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8)) return launch256p_m<0>(p, s);
+  if (lean && !(p.epi_lds & 4) && !(p.bias == nullptr && p.residual == nullptr)) return launch256p_m<1>(p, s);
+  if (p.act != CULLAVO_ACT_NONE && p.act != CULLAVO_ACT_SWIGLU_BWD && p.preact == nullptr && p.addend == nullptr &&
+      p.residual == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store && !(p.epi_lds & 16))
+    return launch256p_m<2>(p, s);
+  return -1;
+}
+
 // Split-K plan for the register-staged kernel: products whose 128x128 tile grid cannot fill
 // the 256 CUs but whose K is long (the LoRA adapter GEMMs: N or M = r = 64, K = tokens or
 // features) are cut into K chunks of >= 4 K-tiles, enough of them for ~512 workgroups.
@@ -476,9 +644,9 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 28);
-  g_epi_lds = lds_staged & 29;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
-                                // activation + SwiGLU-backward paths
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 60);
+  g_epi_lds = lds_staged & 61;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
+                                // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }
@@ -671,6 +839,11 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
   if (tile == kT256x256) {
 #define L256(AL, BL) \
   return f32 ? launch256<AL, BL, CULLAVO_DT_F32, 256, 256>(p, s) : launch256<AL, BL, CULLAVO_DT_BF16, 256, 256>(p, s);
+    if (a_layout == 0 && b_layout == 0 && !f32 && g_persist && p.part == nullptr && p.epi_lds && p.dma_pre &&
+        !(g_epi_lds & 32)) {
+      const int rc = launch256p(p, s);
+      if (rc != -1) return rc;
+    }
     if (a_layout == 0 && b_layout == 0) { L256(0, 0) }
     if (a_layout == 0 && b_layout == 1) { L256(0, 1) }
     if (a_layout == 1 && b_layout == 0) { L256(1, 0) }

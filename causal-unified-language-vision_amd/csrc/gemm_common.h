@@ -379,6 +379,67 @@ DEV void store8(const GemmArgs& p, const float (&a)[8], int64_t m, int64_t n) {
 // 8 contiguous columns each, so every global access is a full-width 16-B access and 32 lanes
 // cover one 512-B output row (the per-lane 8-B stores of the MFMA layout touch 16 rows per
 // instruction; measured +3-4 % on the whole GEMM, tools/lab/gemm_lab.hip).
+// the LDS epilogue's path for this product (lds_epilogue's cases): 0 plain, 1 bias and / or residual,
+// 2 activation, 3 SwiGLU backward, 4 the general store8
+template <int CT>
+DEV int lds_epi_mode(const GemmArgs& p) {
+  const bool lean = CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_NONE && p.preact == nullptr &&
+                    p.addend == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store;
+  if (lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8)) return 0;
+  if (lean && !(p.epi_lds & 4) && !(p.bias == nullptr && p.residual == nullptr)) return 1;
+  if (CT == CULLAVO_DT_BF16 && p.act != CULLAVO_ACT_NONE && p.act != CULLAVO_ACT_SWIGLU_BWD && p.preact == nullptr &&
+      p.addend == nullptr && p.residual == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store &&
+      !(p.epi_lds & 16))
+    return 2;
+  if (CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD && !(p.epi_lds & 16)) return 3;
+  return 4;
+}
+
+// one 8-column group of the LDS epilogue by mode (the arithmetic of store8 in every case)
+template <int CT>
+DEV void lds_store_item(const GemmArgs& p, float (&v)[8], int64_t m, int64_t n, int mode) {
+  if (mode == 4) {
+    store8<CT>(p, v, m, n);
+    return;
+  }
+  if (m >= p.M || n >= p.N) return;
+  if (mode == 3) {
+    swiglu_bwd_store<8>(p, v, m, n);
+    return;
+  }
+  float b[8], rs[8];
+  if (mode != 0 && p.bias) {
+    const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = bf2f(bv[j]);
+  }
+  if (mode == 1 && p.residual) {
+    const u16x8 rv = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs[j] = bf2f(rv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float x = v[j] * p.alpha;
+    if (mode != 0 && p.bias) x += b[j];
+    if (mode == 2) x = round_bf(x);
+    if (mode == 1 && p.residual) x = round_bf(x) + rs[j];
+    v[j] = x;
+  }
+  if (mode == 2) {
+    if (p.act == CULLAVO_ACT_QUICK_GELU) {
+      quick_gelu8(v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
+    }
+  }
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
+}
+
 // item i of a half's LDS image: 8 consecutive f32 outputs of one row (thread idx = tid + 512 i:
 // row idx >> 5, columns (idx & 31) * 8 ..), and their coordinates
 template <int R>
