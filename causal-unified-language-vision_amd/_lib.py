@@ -13,6 +13,10 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcullavo_hip.so")
+# A/B of two builds of the library in one process tree (tools): CULLAVO_LIB_AB names another build of
+# the same ABI; unset, the in-tree library is the only one ever loaded
+if os.environ.get("CULLAVO_LIB_AB"):
+    LIB_PATH = os.environ["CULLAVO_LIB_AB"]
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "cullavo_capi.h")
 
 _CTYPE = {

@@ -476,12 +476,8 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
                     p.addend == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store;
   const bool plain = lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8);
   const bool bias_res = lean && !plain && !(p.epi_lds & 4);
-  // bias_act: an activation without preact / addend / residual / beta (the ViT's fc1 forward);
-  // swiglu: the SwiGLU-backward epilogue of the down_proj dX product (epi_lds bit 4: both off)
-  const bool bias_act = CT == CULLAVO_DT_BF16 && p.act != CULLAVO_ACT_NONE && p.act != CULLAVO_ACT_SWIGLU_BWD &&
-                        p.preact == nullptr && p.addend == nullptr && p.residual == nullptr && p.beta == 0.f &&
-                        p.drop_mode != 3 && !p.nt_store && !(p.epi_lds & 16);
-  const bool swiglu = CT == CULLAVO_DT_BF16 && p.act == CULLAVO_ACT_SWIGLU_BWD && !(p.epi_lds & 16);
+  // (unrolled activation / SwiGLU-backward paths here measured a slower 7B step: every 8-wave
+  // kernel carried their code -- the persistent forward kernel has them per instantiation)
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if (wm == half) {
@@ -536,45 +532,6 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
           }
           *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
         }
-      }
-    } else if (bias_act) {
-#pragma unroll
-      for (int i = 0; i < R * 32 / 512; ++i) {
-        float v[8];
-        int64_t m, n;
-        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
-        if (m < p.M && n < p.N) {
-          float b[8];
-          if (p.bias) {
-            const u16x8 bv = *reinterpret_cast<const u16x8*>(p.bias + n);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) b[j] = bf2f(bv[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float x = v[j] * p.alpha;
-            if (p.bias) x += b[j];
-            v[j] = round_bf(x);
-          }
-          if (p.act == CULLAVO_ACT_QUICK_GELU) {
-            quick_gelu8(v);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
-          }
-          u16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-          *reinterpret_cast<u16x8*>(reinterpret_cast<u16*>(p.C) + m * p.ldc + n) = o;
-        }
-      }
-    } else if (swiglu) {
-#pragma unroll
-      for (int i = 0; i < R * 32 / 512; ++i) {
-        float v[8];
-        int64_t m, n;
-        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
-        if (m < p.M && n < p.N) swiglu_bwd_store<8>(p, v, m, n);
       }
     } else {  // rolled: one copy of the general store8 per half keeps the kernel's code small
 #pragma unroll 1
