@@ -504,6 +504,11 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
              2: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, 1, false>",
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false> split-K + splitk_reduce_k<1>",
              10: f"gemm256_k<{al}, {bl}, 1, 288, 256, 1, {lf}>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
+    ep = os.environ.get("CULLAVO_GEMM_EPILOGUE")
+    if tile == 2 and (al, bl) == (0, 0) and not lora and (ep is None or (int(ep) & 1 and not int(ep) & 32)):
+        # the persistent forward kernel (gemm.hip launch256p), one instantiation per epilogue
+        # mode (0 plain, 1 bias/residual, 2 activation); one block per CU
+        return "gemm256p_k<MODE>", min(int(g.value), 256)  # 256 CUs on MI355X
     if tile >= 100:  # the M-tail split: the head rows' kernel (+ a thin split-K product for the rest)
         return names.get(tile - 100, f"tile{tile - 100}<{al}, {bl}>") + " M-split", int(g.value)
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)

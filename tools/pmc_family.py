@@ -22,10 +22,10 @@ from collections import defaultdict
 
 def per_dispatch(path, kname):
     """counters per dispatch of the kernel whose name (template arguments as rocprofv3 prints
-    them) contains kname"""
+    them) contains kname; "<MODE>" matches every epilogue-mode instantiation of a kernel"""
     d = defaultdict(dict)
     for r in csv.DictReader(open(path)):
-        if kname in r["Kernel_Name"]:
+        if kname.replace("<MODE>", "<") in r["Kernel_Name"]:
             key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(d))
             d[key][r["Counter_Name"]] = d[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return d
