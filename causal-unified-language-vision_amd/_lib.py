@@ -14,9 +14,14 @@ import re
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcullavo_hip.so")
 # A/B of two builds of the library in one process tree (tools): CULLAVO_LIB_AB names another build of
-# the same ABI; unset, the in-tree library is the only one ever loaded
+# the same ABI; unset, the in-tree library is the only one ever loaded. The override is announced on
+# stderr (a stray variable must not silently change the kernels a run uses), and lib() still checks the
+# build's ABI against the header
 if os.environ.get("CULLAVO_LIB_AB"):
     LIB_PATH = os.environ["CULLAVO_LIB_AB"]
+    import sys as _sys
+    print(f"cullavo_amd: CULLAVO_LIB_AB is set, loading {LIB_PATH} instead of the in-tree library",
+          file=_sys.stderr, flush=True)
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "cullavo_capi.h")
 
 _CTYPE = {

@@ -582,7 +582,9 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_
     const double t = seconds(c, M);
     if (t < best * 0.999) { best = t; bid = c.id; }
     const int64_t mm = M / c.bm * c.bm;
-    if (m_main && g_msplit && c.id != kT128 && mm > 0 && mm < M) {
+    // the remaining rows run as a product of their own: keep them above the decode-row sizes (a tail
+    // of <= 16 rows would reach kernels with an M > 16 requirement, e.g. the fused LoRA up-projection)
+    if (m_main && g_msplit && c.id != kT128 && mm > 0 && M - mm > 16) {
       const double ts = seconds(c, mm) + rem_seconds(M - mm, N, K);
       if (ts < best_split * 0.999) { best_split = ts; bid_split = c.id; mm_split = mm; }
     }

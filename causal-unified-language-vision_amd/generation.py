@@ -139,7 +139,8 @@ def layer_infer(layer, h, sctx: StepContext, cache: KVCache, li: int, Lnew: int,
     # round-4 per-fragment form was ~2x slower, profiles/r04/decode/decode_fusions_ab.txt) for the
     # rows that fit LDS (M (d + 8) * 2 <= 64 KiB); FUSE_DECODE_SWIGLU: the SwiGLU in down_proj's
     # X loads (transform 2), only without FUSE_DECODE_GU. All bitwise the unfused values.
-    fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] * (d + 8) * 2 <= 65536 and h.dtype == torch.bfloat16
+    fused = (FUSE_DECODE_NORMS and Lnew == 1 and h.shape[0] <= 16 and h.shape[0] * (d + 8) * 2 <= 65536
+             and h.dtype == torch.bfloat16
              and all(g is NO_LORA for g in lg.values()))
     if fused:
         qkv = ops.decode_linear(h, layer.w_qkv(), transform=1, norm_w=layer.input_layernorm.weight,

@@ -7,6 +7,7 @@ between the read and its wait would use stale values (round 4: a spill store of 
 transposed fragments in the pipelined forward's tail gave wrong rows). Disassembles the device
 code of libcullavo_hip.so with llvm-objdump and scans every LDS read of those kernels forward to
 the first lgkmcnt wait."""
+import functools
 import os
 import re
 import shutil
@@ -40,6 +41,7 @@ def _operands(ins):
     return parts[0], parts[1:]
 
 
+@functools.lru_cache(maxsize=1)
 def _kernels():
     tmp = tempfile.mkdtemp()
     try:
@@ -62,7 +64,8 @@ def _kernels():
                         out[name] = body
                     name, body = m.group(1), []
                 elif name and line.startswith("\t"):
-                    body.append(line.split("//")[0].strip())
+                    am = re.search(r"//\s*([0-9A-Fa-f]+):", line)
+                    body.append((int(am.group(1), 16) if am else -1, line.split("//")[0].strip()))
             if name:
                 out[name] = body
         return out
@@ -99,6 +102,79 @@ def _early_uses(body, allow_branch=False):
     return bad
 
 
+# the dK/dV kernels that store dS^T while the next tile's LDS-DMA is in flight (DS_OUT = DMA = true):
+# their loop ends with a hand-counted `s_waitcnt vmcnt(4)` that lets exactly the tile's four dS^T stores
+# stay outstanding (attention.hip, the DMA branch at the end of the tile loop)
+DS_OUT_DMA_KERNELS = ("attn_bwd_dkdv8_kILi128ELb1ELb1ELb1E", "attn_bwd_dkdv8_kILi128ELb0ELb1ELb1E",
+                      "attn_bwd_dkdv8_kILi64ELb1ELb1ELb1E", "attn_bwd_dkdv8_kILi64ELb0ELb1ELb1E")
+
+
+def _counted_vmcnt_problems(body, n=4):
+    """every `s_waitcnt vmcnt(n)` must have, on EVERY control-flow path into it, at least n
+    vector-memory STORES issued after the last vector-memory load (the LDS-DMA pieces and the aux
+    loads are then retired by the wait); a load among the n youngest (the compiler reordering a load
+    behind the stores) is a silent race. Paths are followed backwards through fall-through edges and
+    SOPP branches (target = pc + 4 + 4 * simm16)."""
+    index = {addr: i for i, (addr, _) in enumerate(body)}
+    preds = {i: [] for i in range(len(body))}
+    for i, (addr, ins) in enumerate(body):
+        op = ins.split()[0] if ins else ""
+        if op.startswith("s_cbranch") or op == "s_branch":
+            simm = int(ins.split()[1])
+            simm = simm - 65536 if simm >= 32768 else simm
+            t = index.get(addr + 4 + 4 * simm)
+            if t is not None:
+                preds[t].append(i)
+        if op not in ("s_branch", "s_endpgm", "s_setpc_b64") and i + 1 < len(body):
+            preds[i + 1].append(i)
+
+    def min_stores(start):
+        best = None
+        seen = set()
+        stack = [(p, 0) for p in preds[start]]
+        while stack:
+            j, cnt = stack.pop()
+            if (j, cnt) in seen or cnt > n:
+                continue
+            seen.add((j, cnt))
+            op = body[j][1].split()[0] if body[j][1] else ""
+            if op.startswith(("global_store", "buffer_store", "scratch_store", "flat_store")):
+                cnt += 1
+            elif op.startswith(("global_load", "buffer_load", "scratch_load", "flat_load", "global_atomic",
+                                "buffer_atomic")):
+                best = cnt if best is None else min(best, cnt)
+                continue
+            if cnt >= n:
+                continue  # enough stores on this path already
+            stack.extend((p, cnt) for p in preds[j])
+        return n if best is None else best
+
+    bad = []
+    for i, (_, ins) in enumerate(body):
+        if re.match(rf"s_waitcnt vmcnt\({n}\)", ins):
+            m = min_stores(i)
+            if m < n:
+                bad.append((i, ins, f"a path with {m} stores after its last load"))
+    return bad
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
+def test_dkdv_dsout_counted_vmcnt_leaves_only_the_stores():
+    """the LDS-DMA dK/dV kernel's `vmcnt(4)` assumes the four dS^T stores are the only
+    vector-memory ops issued after the next tile's DMA and aux loads; checked on the built code."""
+    kernels = _kernels()
+    checked = [n for n in kernels if any(k in n for k in DS_OUT_DMA_KERNELS)]
+    assert len(checked) == len(DS_OUT_DMA_KERNELS), checked
+    problems = {}
+    for n in checked:
+        waits = [ins for _, ins in kernels[n] if re.match(r"s_waitcnt vmcnt\(4\)", ins)]
+        assert waits, f"{n}: no vmcnt(4) wait found"
+        bad = _counted_vmcnt_problems(kernels[n])
+        if bad:
+            problems[n] = bad[:3]
+    assert not problems, problems
+
+
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
 def test_inline_asm_lds_reads_not_used_before_their_wait():
     kernels = _kernels()
@@ -106,7 +182,7 @@ def test_inline_asm_lds_reads_not_used_before_their_wait():
     assert any("attn_fwd_pipe_k" in n for n in checked) and any("attn_fwd_kILi128ELb1ELi5E" in n for n in checked)
     problems = {}
     for n in checked:
-        bad = _early_uses(kernels[n], allow_branch=False)
+        bad = _early_uses([ins for _, ins in kernels[n]], allow_branch=False)
         if bad:
             problems[n] = bad[:3]
     assert not problems, problems

@@ -293,6 +293,39 @@ def test_lora_fused_into_base_gemm(T, epi):
     close(outs[True][0], z, 1.5e-2, f"fused LoRA {epi}")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [16 * 288 + 8, 16 * 288 + 17])
+def test_lora_fused_msplit_short_tail(T):
+    """The M-tail split never hands a fused-LoRA product a tail of <= 16 rows (o_proj /
+    down_proj with LoRA at M = 16 x 288 + 8 took the split and the tail's fused LoRA rejected M <= 16).
+    The plan keeps such M whole; a 17-row tail may split. Fused equals the unfused path to one bf16
+    step either way."""
+    import ctypes
+    from cullavo_amd import _lib, ops
+    inn, out, r, n = 4096, 4096, 64, 1
+    L = _lib.lib()
+    plan = L.cullavo_gemm_plan(T, n * out, inn, 0, 0, ctypes.byref(ctypes.c_int64(0)))
+    if T % 288 <= 16:
+        assert plan < 100, plan  # no split with a <= 16-row tail
+    ar, grp, s, names = _lora_arena(n, out, inn, r, 70)
+    x = rnd((T, inn), 71).cuda()
+    W = rnd((n * out, inn), 72, inn ** -0.5).cuda()
+    res = rnd((T, n * out), 73).cuda()
+    term, u = grp.forward(x, False, 0)
+    assert term.fused_args(T, n * out) is not None
+    outs = {}
+    for fuse in (True, False):
+        prev = ops.LORA_FUSE
+        ops.LORA_FUSE = fuse
+        try:
+            outs[fuse] = ops.linear(x, W, None, residual=res, addend=term)
+        finally:
+            ops.LORA_FUSE = prev
+    d = (outs[True].float() - outs[False].float()).abs()
+    assert d.max().item() <= 2 ** -7 * max(1.0, outs[False].float().abs().max().item()), d.max().item()
+    assert (d != 0).float().mean().item() < 0.01
+
+
 def _lora_oracle_masks(model, sctx_seed, n_tokens):
     """The masks the model's LM adapters draw for one forward (vision tower runs in eval)."""
     from cullavo_amd.lora import module_seed
