@@ -46,12 +46,17 @@ def main():
         fl = 2.0 * M * N * K
         res = {v: [] for v in variants}
         errs = {}
+        first = None
+        same = {}
         for v in variants:
-            C.zero_()
+            C.fill_(float("nan"))
             rc = lib.lab_gemm(v, M, N, K, A.data_ptr(), B.data_ptr(), C.data_ptr(), stream)
             assert rc == 0, (v, rc)
             torch.cuda.synchronize()
             errs[v] = ((C.float() - ref).norm() / ref.norm()).item()
+            if first is None:
+                first = C.clone()
+            same[v] = bool(torch.equal(C, first))
         tb, tp = [], []
         if prod is not None:
             yp = prod.linear(A, B)
@@ -86,7 +91,7 @@ def main():
         if tp:
             line += f" | prod {statistics.median(tp):7.1f} (err {errs['prod']:.1e})"
         for v in variants:
-            line += f" | v{v} {statistics.median(res[v]):7.1f} (err {errs[v]:.1e})"
+            line += f" | v{v} {statistics.median(res[v]):7.1f} (err {errs[v]:.1e}{'' if same[v] else ' DIFF'})"
         print(line, flush=True)
 
 
