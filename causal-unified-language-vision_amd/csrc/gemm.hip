@@ -195,7 +195,9 @@ DEV void lora_fuse(GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int staged, i
   p.bias = nullptr;
 }
 
-template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0, bool LORA = false>
+// EPI > 0: the direct epilogue (direct_epilogue, lean case EPI - 1) instead of the LDS-staged one,
+// chosen by the host per product (launch256_lean)
+template <int AL, int BL, int CT, int BMT, int BN, int LDR = 0, bool LORA = false, bool SWG = false, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
   constexpr int BM2 = BMT;  // 256 or 192 (192 only with a K-contiguous A)
   constexpr int WN_COLS = BN / 4;     // per-wave N extent (4 waves across N)
@@ -237,6 +239,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_k(GemmArgs p) {
                                                                        lane, acc);
   if constexpr (LORA) lora_fuse<BM2, BN, TMW, TN>(p, acc, smem, staged, m0, n0, wave, wm, wn, lane);
 
+  if constexpr (EPI > 0 && BN == 256) {
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const u16*)p.C, ((p.M - 1) * p.ldc + p.N) * 2);
+    direct_epilogue<EPI - 1, TMW>(p, acc, rc, m0 + wm * (BM2 / 2), n0 + wn * WN_COLS, lane);
+    return;
+  }
+  if constexpr (SWG) {  // launched only with act 3, the LDS epilogue on and a bf16 C (launch256_swiglu)
+    lds_epilogue_swiglu<CT, BM2, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
+    return;
+  }
   if constexpr (BN == 256) {
     if (p.epi_lds) {
       lds_epilogue<CT, BM2, TMW, TN>(p, acc, smem, m0, n0, wm, wn, lane);
@@ -393,6 +404,110 @@ __global__ __launch_bounds__(512, 1) void gemm256p_k(GemmArgs p) {
   }
 }
 
+// ---- persistent forward kernel with the direct epilogue (round 6) ------------------------------
+// gemm256p_k's tile walk and K-loop, with (a) the epilogue written straight from the accumulators by
+// direct_epilogue (permlane16-widened 16-B buffer stores, no LDS round trip, no barrier), (b) the next
+// tile's K-tile 1 issued by the loader waves BEFORE those stores (into the stage this tile's last
+// K-tile freed), so the stores drain under the next tile's K-tile 0 (the loaders' first wait is a
+// counted vmcnt(2 TMW): every wave issues exactly 16 buffer stores), and (c) the per-piece DMA
+// offsets as one lane base + a scalar row stride behind an opaque copy (rows past M land past the
+// buffer's num_records), which keeps 16 offset registers out of the K-loop. Lab:
+// tools/lab/gemm_hc_lab.hip variant 2 (profiles/r06/gemm/hc_lab.txt): ViT K = 1024 products +5-9 %,
+// gate|up / lm_head +2-3 % over gemm256p_k.
+DEV unsigned dma_base0(int64_t ld, int64_t idx0, int lw, int lane) {
+  const int row = lw * 8 + (lane >> 3);
+  const int chunk = (lane & 7) ^ ((row >> 1) & 7);  // the same for every piece (+32 rows)
+  return (unsigned)(((idx0 + row) * ld + chunk * 8) * 2);
+}
+
+DEV void dma_issue_stride(__amdgpu_buffer_rsrc_t rsrc, unsigned base, unsigned step, int soff, char* lds, int lw) {
+  unsigned off = base;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (lw + 4 * i) * 1024), 16, off, soff, 0, 0);
+    off += step;
+    asm volatile("" : "+v"(off));  // no precomputed per-piece offsets live across the K-loop
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void gemm256pd_k(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const bool loader = wave < 4;
+  const int lw = wave & 3;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int nk = (int)cdiv(p.K, BK);
+  int t = blockIdx.x;
+  if (t >= tiles) return;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, ((p.M - 1) * p.lda + p.K) * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B, ((p.N - 1) * p.ldb + p.K) * 2);
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc((const u16*)p.C, ((p.M - 1) * p.ldc + p.N) * 2);
+  const unsigned step_a = (unsigned)(32 * p.lda * 2), step_b = (unsigned)(32 * p.ldb * 2);
+  PTile xy = ptile(p, xcd_remap(t, p.sk_dp));
+  int64_t m0 = (int64_t)xy.tm * 256, n0 = (int64_t)xy.tn * 256;
+  if (loader) {
+    dma_issue_stride(ra, dma_base0(p.lda, m0, lw, lane), step_a, 0, smem, lw);
+    dma_issue_stride(rb, dma_base0(p.ldb, n0, lw, lane), step_b, 0, smem + P_TA, lw);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  praw_barrier();
+  int s = 0;
+  bool k1_early = false;  // this tile's K-tile 1 went out before the previous tile's stores
+  f32x4 acc[8][4];
+  for (;;) {
+    const int t1 = t + (int)gridDim.x;
+    const bool has_next = t1 < tiles;
+    const PTile xy1 = ptile(p, xcd_remap(has_next ? t1 : t, p.sk_dp));
+    const int64_t m1 = (int64_t)xy1.tm * 256, n1 = (int64_t)xy1.tn * 256;
+    unsigned ba = dma_base0(p.lda, m0, lw, lane), bb = dma_base0(p.ldb, n0, lw, lane);
+    asm volatile("" : "+v"(ba), "+v"(bb));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = smem + ((s + kt) & 1) * P_STAGE;
+      char* nxt = smem + ((s + kt + 1) & 1) * P_STAGE;
+      if (loader && !(kt == 0 && k1_early)) {
+        if (kt + 1 < nk) {
+          const int64_t k1 = (int64_t)(kt + 1) * BK;
+          dma_issue_stride(ra, ba, step_a, dma_soff<0>(k1, p.lda), nxt, lw);
+          dma_issue_stride(rb, bb, step_b, dma_soff<0>(k1, p.ldb), nxt + P_TA, lw);
+        } else if (has_next) {  // the next tile's first K-tile under this tile's last MFMAs
+          unsigned b1a = dma_base0(p.lda, m1, lw, lane), b1b = dma_base0(p.ldb, n1, lw, lane);
+          asm volatile("" : "+v"(b1a), "+v"(b1b));
+          dma_issue_stride(ra, b1a, step_a, 0, nxt, lw);
+          dma_issue_stride(rb, b1b, step_b, 0, nxt + P_TA, lw);
+        }
+      }
+      tile_mfma<0, 0, 256, 256, 8, 4>(cur, wm, wn, lane, acc);
+      // K-tile 0 after an early K-tile 1: the previous tile's 16 stores (issued after that DMA) may
+      // stay in flight; otherwise everything this wave issued has landed
+      if (kt == 0 && k1_early) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      praw_barrier();
+    }
+    // every wave is past the last K-tile's barrier: its stage is free for the next tile's K-tile 1
+    k1_early = has_next && nk > 1;
+    if (k1_early && loader) {
+      char* st1 = smem + ((s + nk + 1) & 1) * P_STAGE;
+      unsigned b1a = dma_base0(p.lda, m1, lw, lane), b1b = dma_base0(p.ldb, n1, lw, lane);
+      asm volatile("" : "+v"(b1a), "+v"(b1b));
+      dma_issue_stride(ra, b1a, step_a, dma_soff<0>(BK, p.lda), st1, lw);
+      dma_issue_stride(rb, b1b, step_b, dma_soff<0>(BK, p.ldb), st1 + P_TA, lw);
+    }
+    direct_epilogue<MODE, 8>(p, acc, rc, m0 + wm * 128, n0 + wn * 64, lane);
+    if (!has_next) break;
+    s = (s + nk) & 1;
+    t = t1;
+    m0 = m1;
+    n0 = n1;
+  }
+}
+
 int g_persist = 1;  // cullavo_gemm_set_epilogue bit 5 turns the persistent forward kernel off (A/B)
 
 template <int MODE>
@@ -411,17 +526,51 @@ int launch256p_m(GemmArgs p, hipStream_t s) {
   return cullavo_check_launch("gemm256 persistent");
 }
 
-// the persistent kernel for the lean epilogue cases (plain, bias / residual, activation); -1: none
-int launch256p(const GemmArgs& p, hipStream_t s) {
-  // lds_epi_mode on the host: the same conditions
+template <int MODE>
+int launch256pd_m(GemmArgs p, hipStream_t s) {
+  const int smem = 2 * P_STAGE;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm256pd_k<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_n = (int)cdiv(p.N, 256);
+  p.sk_dp = p.tiles_m * p.tiles_n;
+  const int grid = std::min(p.sk_dp, num_cus());
+  gemm256pd_k<MODE><<<(unsigned)grid, 512, smem, s>>>(p);
+  return cullavo_check_launch("gemm256 persistent direct");
+}
+
+// the lean epilogue case of a product (lds_epi_mode's 0 plain, 1 bias / residual, 2 activation), or
+// -1 (the general path); on the host, the same conditions
+int lean_mode(const GemmArgs& p) {
   const bool lean = p.act == CULLAVO_ACT_NONE && p.preact == nullptr && p.addend == nullptr && p.beta == 0.f &&
                     p.drop_mode != 3 && !p.nt_store;
-  if (lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8)) return launch256p_m<0>(p, s);
-  if (lean && !(p.epi_lds & 4) && !(p.bias == nullptr && p.residual == nullptr)) return launch256p_m<1>(p, s);
+  if (lean && p.bias == nullptr && p.residual == nullptr && !(p.epi_lds & 8)) return 0;
+  if (lean && !(p.epi_lds & 4) && !(p.bias == nullptr && p.residual == nullptr)) return 1;
   if (p.act != CULLAVO_ACT_NONE && p.act != CULLAVO_ACT_SWIGLU_BWD && p.preact == nullptr && p.addend == nullptr &&
       p.residual == nullptr && p.beta == 0.f && p.drop_mode != 3 && !p.nt_store && !(p.epi_lds & 16))
-    return launch256p_m<2>(p, s);
+    return 2;
   return -1;
+}
+
+// C addressable by one buffer descriptor (the direct epilogue's stores)
+bool c_fits_rsrc(const GemmArgs& p) { return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB; }
+
+// the persistent kernel for the lean epilogue cases (plain, bias / residual, activation); -1: none.
+// cullavo_gemm_set_epilogue bit 7 keeps the LDS-staged epilogue (gemm256p_k) for A/B
+int launch256p(const GemmArgs& p, hipStream_t s) {
+  const int mode = lean_mode(p);
+  if (mode < 0) return -1;
+  if (!(p.epi_lds & 128) && c_fits_rsrc(p)) {
+    if (mode == 0) return launch256pd_m<0>(p, s);
+    if (mode == 1) return launch256pd_m<1>(p, s);
+    return launch256pd_m<2>(p, s);
+  }
+  if (mode == 0) return launch256p_m<0>(p, s);
+  if (mode == 1) return launch256p_m<1>(p, s);
+  return launch256p_m<2>(p, s);
 }
 
 // Split-K plan for the register-staged kernel: products whose 128x128 tile grid cannot fill
@@ -497,13 +646,13 @@ int num_cus() {
 }
 
 
-template <int AL, int BL, int CT, int BM2, int BN2, bool LORA = false>
+template <int AL, int BL, int CT, int BM2, int BN2, bool LORA = false, bool SWG = false, int EPI = 0>
 int launch256(GemmArgs p, hipStream_t s) {
   // two K-tile stages; the LDS-staged epilogue needs BM2/2 f32 rows of 1 KiB (288 rows: 144 KiB)
-  const int smem = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 ? BM2 / 2 * 1024 : 0);
+  const int smem = std::max(2 * (BM2 * BK * 2 + BN2 * BK * 2), BN2 == 256 && EPI == 0 ? BM2 / 2 * 1024 : 0);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA>,
+    (void)hipFuncSetAttribute((const void*)gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA, SWG, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
@@ -513,13 +662,25 @@ int launch256(GemmArgs p, hipStream_t s) {
   p.sk_dp = (int)tiles;
   if (p.part) {  // split-K over the 8-wave kernel (small grids, splitk256_plan), then the reduce
     const int splits = (int)cdiv(nk, p.kt_per);
-    gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
+    gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA, SWG, EPI><<<dim3((unsigned)tiles, splits), 512, smem, s>>>(p);
     const int64_t work = p.M * (p.N / 4);
     splitk_reduce_k<CT><<<(int)std::min<int64_t>(cdiv(work, 256), 4096), 256, 0, s>>>(p, splits);
     return cullavo_check_launch("gemm256 split-K");
   }
-  gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA><<<(unsigned)tiles, 512, smem, s>>>(p);
+  gemm256_k<AL, BL, CT, BM2, BN2, 1, LORA, SWG, EPI><<<(unsigned)tiles, 512, smem, s>>>(p);
   return cullavo_check_launch("gemm256");
+}
+
+// the data-parallel 8-wave kernel with the direct epilogue for the lean plain (EPI 1) and bias /
+// residual (EPI 2) cases of the step's 7B shapes (forward / dX at 288 rows, dX / dW at 256 rows); -1
+// when the product is not one of them (the LDS-staged general epilogue then runs)
+template <int AL, int BL, int BM2>
+int launch256_lean(const GemmArgs& p, hipStream_t s) {
+  if (p.part != nullptr || !p.epi_lds || (p.epi_lds & 128) || !c_fits_rsrc(p)) return -1;
+  const int mode = lean_mode(p);
+  if (mode == 0) return launch256<AL, BL, CULLAVO_DT_BF16, BM2, 256, false, false, 1>(p, s);
+  if (mode == 1) return launch256<AL, BL, CULLAVO_DT_BF16, BM2, 256, false, false, 2>(p, s);
+  return -1;
 }
 
 // Kernel-shape choice. Time model = FLOPs / (per-tile rate of the shape) x (whole rounds of
@@ -646,9 +807,11 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 60);
-  g_epi_lds = lds_staged & 61;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
-                                // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 252);
+  g_epi_lds = lds_staged & 253;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
+                                 // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel;
+                                 // bit 6 the prefetching SwiGLU-backward instantiation; bit 7 the direct
+                                 // (register) epilogue of the lean cases
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }
@@ -800,6 +963,7 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
     p.lora_out = d.lora_out;
     p.lora_scale = d.lora_scale;
     // the 288-row tile where the plan takes it (the N = 4096 products: 2 rounds instead of 3)
+    // (the direct epilogue is not used here: beside the fused LoRA's registers it spills ~100 VGPRs)
     if (choose_tile(M, N, K, 0, g_force_tile) == kT288x256)
       return launch256<0, 0, CULLAVO_DT_BF16, 288, 256, true>(p, s);
     return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, true>(p, s);
@@ -828,7 +992,21 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
     if (a_layout == 0) return f32 ? launch<0, 1, CULLAVO_DT_F32, 2>(p, s) : launch<0, 1, CULLAVO_DT_BF16, 2>(p, s);
     return f32 ? launch<1, 1, CULLAVO_DT_F32, 2>(p, s) : launch<1, 1, CULLAVO_DT_BF16, 2>(p, s);
   }
+  // the SwiGLU-backward dX (act 3, bf16, LDS epilogue on, not split): its own instantiation with the
+  // prefetching epilogue (lds_epilogue_swiglu); cullavo_gemm_set_epilogue bit 6 keeps the general path
+  if (act == CULLAVO_ACT_SWIGLU_BWD && !f32 && p.epi_lds && p.part == nullptr && !(g_epi_lds & 64) &&
+      a_layout == 0 && (tile == kT288x256 || tile == kT256x256)) {
+    if (tile == kT288x256)
+      return b_layout == 0 ? launch256<0, 0, CULLAVO_DT_BF16, 288, 256, false, true>(p, s)
+                           : launch256<0, 1, CULLAVO_DT_BF16, 288, 256, false, true>(p, s);
+    return b_layout == 0 ? launch256<0, 0, CULLAVO_DT_BF16, 256, 256, false, true>(p, s)
+                         : launch256<0, 1, CULLAVO_DT_BF16, 256, 256, false, true>(p, s);
+  }
   if (tile == kT288x256) {  // a_layout 0 (above), one loader wave per SIMD
+    if (!f32) {
+      const int rc = b_layout == 0 ? launch256_lean<0, 0, 288>(p, s) : launch256_lean<0, 1, 288>(p, s);
+      if (rc != -1) return rc;
+    }
     if (b_layout == 0)
       return f32 ? launch256<0, 0, CULLAVO_DT_F32, 288, 256>(p, s) : launch256<0, 0, CULLAVO_DT_BF16, 288, 256>(p, s);
     return f32 ? launch256<0, 1, CULLAVO_DT_F32, 288, 256>(p, s) : launch256<0, 1, CULLAVO_DT_BF16, 288, 256>(p, s);
@@ -844,6 +1022,14 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
     if (a_layout == 0 && b_layout == 0 && !f32 && g_persist && p.part == nullptr && p.epi_lds && p.dma_pre &&
         !(g_epi_lds & 32)) {
       const int rc = launch256p(p, s);
+      if (rc != -1) return rc;
+    }
+    if (!f32 && a_layout == 0 && b_layout == 1) {
+      const int rc = launch256_lean<0, 1, 256>(p, s);
+      if (rc != -1) return rc;
+    }
+    if (!f32 && a_layout == 1 && b_layout == 1) {
+      const int rc = launch256_lean<1, 1, 256>(p, s);
       if (rc != -1) return rc;
     }
     if (a_layout == 0 && b_layout == 0) { L256(0, 0) }

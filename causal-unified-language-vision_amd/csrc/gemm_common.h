@@ -204,6 +204,20 @@ DEV int xcd_remap(int bid, int nwg) {
 // swiglu_bwd_k (elementwise.hip) so the fused and unfused paths are bitwise equal.
 DEV float sigmoid_ieee(float x) { return 1.f / (1.f + __expf(-x)); }
 
+// the arithmetic of one lane's NV columns: dg -> oa, du -> ob (shared by every SwiGLU-backward path)
+template <int NV, typename UV>
+DEV void swiglu_bwd_math(const float* acc, float alpha, const UV& gv, const UV& uv, UV& oa, UV& ob) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const float dv = round_bf(acc[j] * alpha);
+    const float g = bf2f(gv[j]), u = bf2f(uv[j]);
+    const float sg = sigmoid_ieee(g);
+    const float silu = g * sg;
+    ob[j] = f2bf(dv * round_bf(silu));
+    oa[j] = f2bf(dv * u * sg * (1.f + g * (1.f - sg)));
+  }
+}
+
 template <int NV>
 DEV void swiglu_bwd_store(const GemmArgs& p, const float* acc, int64_t m, int64_t n) {
   typedef __attribute__((ext_vector_type(NV))) unsigned short uv_t;
@@ -211,15 +225,7 @@ DEV void swiglu_bwd_store(const GemmArgs& p, const float* acc, int64_t m, int64_
   const uv_t gv = *reinterpret_cast<const uv_t*>(gr + n);
   const uv_t uv = *reinterpret_cast<const uv_t*>(gr + p.N + n);
   uv_t oa, ob;
-#pragma unroll
-  for (int j = 0; j < NV; ++j) {
-    const float dv = round_bf(acc[j] * p.alpha);
-    const float g = bf2f(gv[j]), u = bf2f(uv[j]);
-    const float sg = sigmoid_ieee(g);
-    const float silu = g * sg;
-    ob[j] = f2bf(dv * round_bf(silu));
-    oa[j] = f2bf(dv * u * sg * (1.f + g * (1.f - sg)));
-  }
+  swiglu_bwd_math<NV>(acc, p.alpha, gv, uv, oa, ob);
   u16* cp = (u16*)p.C + m * p.ldc + n;
   *reinterpret_cast<uv_t*>(cp) = oa;
   *reinterpret_cast<uv_t*>(cp + p.N) = ob;
@@ -459,6 +465,72 @@ DEV void lds_epi_item(const char* smem, int i, int half, int64_t m0, int64_t n0,
   n = n0 + pr * 8;
 }
 
+// SWG: the instantiation for the SwiGLU-backward epilogue only (act 3, bf16; gemm256_k<..., SWG = true>,
+// chosen by the host for that act): per row half, every item's g and u rows (16 B each) are loaded
+// BEFORE the half's accumulators are staged in LDS, so the loads' latency runs under the staging and
+// the barrier, and the items are unrolled (the general path below is a rolled loop whose every item
+// waited for its own two dependent loads: the 8704 x 11008 x 4096 dX ran at 1021 against 1274 TF/s
+// plain). Same arithmetic as swiglu_bwd_store (swiglu_bwd_math): bitwise.
+template <int CT, int BM2, int TMW, int TN>
+DEV void lds_epilogue_swiglu(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wm,
+                             int wn, int lane) {
+  constexpr int R = BM2 / 2;
+  constexpr int NI = R * 32 / 512;       // items per thread and half: 9 (288 rows) or 8 (256)
+  constexpr int NB = NI % 3 == 0 ? 3 : 4;  // items per batch: one batch's loads in flight ahead
+  u16x8 gv[NI], uv[NI];
+  auto load = [&](int half, int i) {
+    const int idx = threadIdx.x + 512 * i;
+    const int64_t m = m0 + half * R + (idx >> 5), n = n0 + (idx & 31) * 8;
+    if (m < p.M && n < p.N) {
+      const u16* gr = p.residual + m * p.ldr + n;
+      gv[i] = *reinterpret_cast<const u16x8*>(gr);
+      uv[i] = *reinterpret_cast<const u16x8*>(gr + p.N);
+    }
+  };
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    // the first batch's loads fly under the staging (sched_barriers keep the compiler from hoisting
+    // later batches' loads: with the other half's accumulators live, more would spill)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) load(half, i);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == half) {
+#pragma unroll
+      for (int tm = 0; tm < TMW; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const int r = tm * 16 + (lane & 15);
+          const int c = wn * 16 + tn * 4 + (lane >> 4);
+          *reinterpret_cast<f32x4*>(smem + r * 1024 + ((c ^ (r & 15)) << 4)) = acc[tm][tn];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NI; b += NB) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + NB < NI) {
+#pragma unroll
+        for (int i = b + NB; i < b + 2 * NB && i < NI; ++i) load(half, i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = b; i < b + NB; ++i) {
+        float v[8];
+        int64_t m, n;
+        lds_epi_item<R>(smem, i, half, m0, n0, v, m, n);
+        if (m < p.M && n < p.N) {
+          u16x8 oa, ob;
+          swiglu_bwd_math<8>(v, p.alpha, gv[i], uv[i], oa, ob);
+          u16* cp = (u16*)p.C + m * p.ldc + n;
+          *reinterpret_cast<u16x8*>(cp) = oa;
+          *reinterpret_cast<u16x8*>(cp + p.N) = ob;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int CT, int BM2, int TMW, int TN>
 DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int64_t m0, int64_t n0, int wm,
                       int wn, int lane) {
@@ -543,6 +615,98 @@ DEV void lds_epilogue(const GemmArgs& p, f32x4 (&acc)[TMW][TN], char* smem, int6
       }
     }
     __syncthreads();
+  }
+}
+
+// ============================================================================================
+// Direct epilogue (round 6): the tile's C straight from the accumulators, no LDS round trip
+// ============================================================================================
+// In the 16x16 MFMA layout a lane holds 4 consecutive columns of one row per (tm, tn). Packed to
+// bf16 (two dwords per tile) and swapped with v_permlane16_swap (rows 1 / 3 of the first operand <->
+// rows 0 / 2 of the second, 16-lane rows) between the tiles tn = 2 pr and 2 pr + 1, each lane holds 8
+// consecutive columns: lane group g = lane >> 4 has tile 2 pr + (g & 1), columns 8 (g >> 1) .. + 7.
+// So a wave stores its 16 x 64 block of one tm as two 16-B stores per lane (rows of 2 x 32 B), with
+// no ds_write / ds_read / barrier. Lab (tools/lab/gemm_hc_lab.hip, profiles/r06/gemm/hc_lab.txt):
+// 2-6 % faster than the LDS-staged epilogue in the persistent kernel at equal results.
+// The stores are buffer stores on C's descriptor: an out-of-range row or column gets an offset past
+// num_records and is dropped, so every wave always issues exactly 2 TMW store instructions (the
+// persistent kernel counts them in its vmcnt). MODE: 0 plain, 1 bias and / or residual, 2 activation
+// (after an optional bias) -- lds_epi_mode's cases 0-2, in store8's arithmetic (bitwise).
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4e;
+
+DEV unsigned pk_bf2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+
+template <int MODE, int TMW>
+DEV void direct_epilogue(const GemmArgs& p, const f32x4 (&acc)[TMW][4], __amdgpu_buffer_rsrc_t rc, int64_t wm0,
+                         int64_t wn0, int lane) {
+  const int g = lane >> 4;
+  float bv[4][4];
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[tn][j] = 0.f;
+  if (MODE != 0 && p.bias) {
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int64_t n = wn0 + tn * 16 + g * 4;
+      if (n < p.N) {
+        const u16x4 b4 = *reinterpret_cast<const u16x4*>(p.bias + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[tn][j] = bf2f(b4[j]);
+      }
+    }
+  }
+  const bool res = MODE == 1 && p.residual != nullptr;
+  // this lane's chunk column (after the swap) for pair pr: wn0 + (2 pr + (g & 1)) * 16 + (g >> 1) * 8
+  const int64_t nc0 = wn0 + (g & 1) * 16 + (g >> 1) * 8;
+#pragma unroll
+  for (int tm = 0; tm < TMW; ++tm) {
+    const int64_t m = wm0 + tm * 16 + (lane & 15);
+    u16x8 rv[2];
+    if (res) {  // this tm's two residual chunks (same rows / columns as the stores below)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int64_t n = nc0 + pr * 32;
+        if (m < p.M && n < p.N) rv[pr] = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
+      }
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float v[8];  // this lane's pre-swap values: tile 2 pr columns 0-3, then tile 2 pr + 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x = acc[tm][2 * pr + h][j] * p.alpha;
+          if (MODE != 0) x += bv[2 * pr + h][j];
+          v[h * 4 + j] = x;
+        }
+      if (MODE == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]);
+        if (p.act == CULLAVO_ACT_QUICK_GELU) {
+          quick_gelu8(v);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = act_apply(p.act, v[j]);
+        }
+      }
+      unsigned p0 = pk_bf2(v[0], v[1]), p1 = pk_bf2(v[2], v[3]);
+      unsigned q0 = pk_bf2(v[4], v[5]), q1 = pk_bf2(v[6], v[7]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(p0, q0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(p1, q1, false, false);
+      u32x4e o = u32x4e{s0[0], s1[0], s0[1], s1[1]};
+      const int64_t n = nc0 + pr * 32;
+      const bool in = m < p.M && n < p.N;
+      if (res) {  // store8's round(v) + residual, rounded once more
+        u16x8 w = __builtin_bit_cast(u16x8, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = f2bf(bf2f(w[j]) + (in ? bf2f(rv[pr][j]) : 0.f));
+        o = __builtin_bit_cast(u32x4e, w);
+      }
+      const unsigned off = in ? (unsigned)((m * p.ldc + n) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(o, rc, off, 0, 0);
+    }
   }
 }
 

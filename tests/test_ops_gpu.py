@@ -150,6 +150,55 @@ def test_gemm_epilogue_paths_bit_identical(tile_mode, act):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("M,N,K,al,bl,tile,epi", [
+    (2000, 1032, 1024, 0, 0, 2, "plain"), (2000, 1032, 1024, 0, 0, 2, "bias"), (2000, 1032, 1024, 0, 0, 2, "bias_res"),
+    (2000, 1032, 1024, 0, 0, 2, "qgelu"), (2000, 1032, 1024, 0, 0, 2, "gelu"), (300, 264, 192, 0, 0, 2, "res"),
+    (2000, 1032, 4096, 0, 0, 10, "plain"), (2000, 1032, 4096, 0, 0, 10, "res"), (8704 + 37, 4096, 4096, 0, 0, 10, "res"),
+    (2000, 1032, 4096, 0, 1, 10, "plain"), (2000, 1032, 4096, 0, 1, 10, "res"), (2000, 1032, 1000, 0, 1, 2, "plain"),
+    (2000, 1032, 1000, 0, 1, 2, "res"), (1032, 2056, 2000, 1, 1, 2, "plain"), (1032, 2056, 2000, 1, 1, 2, "res"),
+    # > 256 tiles: the persistent kernel walks several tiles per CU (early K-tile 1 DMA, counted vmcnt)
+    (8704 + 37, 4104, 1024, 0, 0, 2, "bias_res"), (8704 + 37, 2056, 192, 0, 0, 2, "plain"),
+    (8704, 4096, 64, 0, 0, 2, "qgelu"), (8704 + 37, 4104, 1024, 0, 0, 2, "res")])
+def test_gemm_direct_epilogue_bitwise(M, N, K, al, bl, tile, epi):
+    """The direct epilogue (round 6: accumulators packed, permlane16-swapped and stored as 16-B buffer
+    stores, no LDS round trip; the persistent forward kernel with the next tile's K-tile 1 issued
+    before the stores, and the data-parallel 288- / 256-row kernels) against the LDS-staged epilogue
+    (cullavo_gemm_set_epilogue bit 7) and the per-lane epilogue (bit 0 off): bitwise equal for every
+    lean case (plain, bias, residual, bias + residual, quick_gelu / erf-GELU after a bias), ragged M
+    and N tiles included, and within bf16 noise of the fp32 product."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn((K, M) if al else (M, K), device=DEV, generator=g).to(BF)
+    B = (torch.randn((K, N) if bl else (N, K), device=DEV, generator=g) * K ** -0.5).to(BF)
+    bias = (torch.randn(N, device=DEV, generator=g) * 0.5).to(BF) if epi in ("bias", "bias_res", "qgelu", "gelu") else None
+    res = torch.randn(M, N, device=DEV, generator=g).to(BF) if epi in ("res", "bias_res") else None
+    act = {"qgelu": ops().ACT_QUICK_GELU, "gelu": ops().ACT_GELU}.get(epi, ops().ACT_NONE)
+    prev_t, prev_e = L.cullavo_gemm_set_tile(tile), L.cullavo_gemm_set_epilogue(1)
+    outs = []
+    try:
+        for mode in (1, 1 | 128, 0):
+            L.cullavo_gemm_set_epilogue(mode)
+            C = torch.full((M, N), float("nan"), dtype=BF, device=DEV)
+            ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, act=act, residual=res,
+                       ldr=N if res is not None else 0)
+            outs.append(C)
+    finally:
+        L.cullavo_gemm_set_tile(prev_t)
+        L.cullavo_gemm_set_epilogue(prev_e)
+    Ad = A.t() if al else A
+    Bd = B if bl else B.t()
+    ref = (Ad.float() @ Bd.float()) + (bias.float() if bias is not None else 0)
+    if act:
+        ref = ref.to(BF).float()
+        ref = O.quick_gelu(ref) if epi == "qgelu" else F.gelu(ref)
+    if res is not None:
+        ref = ref.to(BF).float() + res.float()
+    close(outs[0], ref, 8e-3, f"direct epilogue {epi}")
+    assert torch.equal(outs[0], outs[1]), "direct vs LDS-staged epilogue"
+    assert torch.equal(outs[0], outs[2]), "direct vs per-lane epilogue"
+
+
 @pytest.mark.parametrize("M,N,K,al,bl", [(2304, 8192, 1024, 0, 0), (1032, 2056, 4104, 1, 1), (2000, 1544, 520, 0, 1),
                                           (1000, 4104, 1032, 1, 0)])
 def test_gemm_tile_order_bitwise(M, N, K, al, bl):
