@@ -484,10 +484,13 @@ __global__ __launch_bounds__(512, 1) void gemm256pd_k(GemmArgs p) {
         }
       }
       tile_mfma<0, 0, 256, 256, 8, 4>(cur, wm, wn, lane, acc);
-      // K-tile 0 after an early K-tile 1: the previous tile's 16 stores (issued after that DMA) may
-      // stay in flight; otherwise everything this wave issued has landed
-      if (kt == 0 && k1_early) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // loaders: K-tile 0 after an early K-tile 1 leaves the previous tile's 16 stores (issued after
+      // that DMA) in flight; otherwise everything the wave issued has landed. The other waves issue
+      // no vector-memory op in the K-loop: they never wait, so their epilogue stores drain under it
+      if (loader) {
+        if (kt == 0 && k1_early) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       praw_barrier();
     }
     // every wave is past the last K-tile's barrier: its stage is free for the next tile's K-tile 1

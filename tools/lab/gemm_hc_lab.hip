@@ -279,7 +279,7 @@ DEV void put_held_from(const GemmArgs& p, const HeldN<H>& h, int64_t hm0, int64_
 
 template <int H, int VAR>
 __global__ __launch_bounds__(512, 1) void gemm_hc_k(GemmArgs p) {
-  constexpr bool SC1 = VAR & 2, NOSTORE = VAR & 4, EARLY = VAR & 1, PRE = VAR & 8;
+  constexpr bool SC1 = VAR & 2, NOSTORE = VAR & 4, EARLY = VAR & 1, PRE = VAR & 8, NLSKIP = VAR & 16;
   constexpr int GROUPS = H / 2;  // K-tiles that drain the held chunks (2 per K-tile)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -351,7 +351,9 @@ __global__ __launch_bounds__(512, 1) void gemm_hc_k(GemmArgs p) {
       const bool storing = H > 0 && !NOSTORE && held && kt < GROUPS;
       if (storing) put_held_step<H>(p, h, hm0, hn0, lane, kt, SC1);
       tile_mfma<0, 0, 256, 256, 8, 4>(cur, wm, wn, lane, acc);
-      if (kt == 0 && pending > 0) {  // the end-of-tile stores (after K-tile 1's DMA) may stay in flight
+      if (NLSKIP && !loader) {
+        // the non-loader waves issue no vector-memory op in the K-loop: their stores drain freely
+      } else if (kt == 0 && pending > 0) {  // the end-of-tile stores (after K-tile 1's DMA) may stay in flight
         constexpr int P = 16 - H;
         if (storing) {
           if constexpr (P + 2 == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
@@ -458,6 +460,8 @@ extern "C" int lab_gemm(int v, int64_t M, int64_t N, int64_t K, const void* A, c
     case 4: return launch(gemm_hc_k<0, 4>, p, st);
     case 5: return launch(gemm_hc_k<0, 8>, p, st);
     case 6: return launch(gemm_hc_k<0, 3>, p, st);
+    case 7: return launch(gemm_hc_k<0, 17>, p, st);   // early DMA + non-loaders never wait
+    case 8: return launch(gemm_hc_k<0, 16>, p, st);   // non-loaders never wait
     case 101: return launch(gemm_hc_k<8, 0>, p, st);
     case 102: return launch(gemm_hc_k<8, 1>, p, st);
     case 103: return launch(gemm_hc_k<8, 2>, p, st);
