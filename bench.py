@@ -505,22 +505,36 @@ def layer_roofline(spans: dict, fl: dict, args, tc):
 def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
     """rocprof name (template arguments as rocprofv3 prints them) + workgroup count of the
     kernel cullavo_gemm picks for a bf16-output problem (cullavo_gemm_plan); lora: the
-    instantiation with the fused LoRA up-projection (gemm256_k<..., LORA = true>)"""
+    instantiation with the fused LoRA up-projection (gemm256_k<..., LORA = true>).
+    gemm256_k<AL, BL, CT, BM, BN, LDR, LORA, SWG, EPI>: EPI 1 / 2 the direct (register) epilogue of
+    plain / bias-residual products, 0 the LDS-staged one. The problem key carries no epilogue, so a
+    forward / dX family whose products differ in it is named with EPI "*" (either of 1, 2; the PMC
+    tools match "*" as a wildcard); the SwiGLU-backward dX (SWG = true) is a family of its own only
+    by rocprof name. "<MODE>": every epilogue-mode instantiation of the persistent kernel."""
     import ctypes
     from cullavo_amd import _lib
     g = ctypes.c_int64(0)
     tile = _lib.lib().cullavo_gemm_plan(M, N, K, al, bl, ctypes.byref(g))
-    # the 256-row kernels' last template argument is the fused-LoRA flag (rocprofv3 prints it)
-    lf = "true" if lora else "false"
-    names = {0: f"gemm_k<{al}, {bl}, 1, 0>",
-             2: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, {lf}>", 3: f"gemm256_k<{al}, {bl}, 1, 192, 256, 1, false>",
-             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false> split-K + splitk_reduce_k<1>",
-             10: f"gemm256_k<{al}, {bl}, 1, 288, 256, 1, {lf}>", 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
     ep = os.environ.get("CULLAVO_GEMM_EPILOGUE")
-    if tile == 2 and (al, bl) == (0, 0) and not lora and (ep is None or (int(ep) & 1 and not int(ep) & 32)):
+    ep = 1 if ep is None else int(ep)
+    direct = bool(ep & 1) and not ep & 128
+    lf = "true" if lora else "false"
+
+    def g256(bm):
+        if lora or not direct or (bm == 192):
+            e = "0"
+        elif (al, bl) == (1, 1):
+            e = "1"  # weight gradients: always plain
+        else:
+            e = "*"
+        return f"gemm256_k<{al}, {bl}, 1, {bm}, 256, 1, {lf}, false, {e}>"
+    names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 2: g256(256), 3: g256(192),
+             9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false, false, 0> split-K + splitk_reduce_k<1>",
+             10: g256(288), 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
+    if tile == 2 and (al, bl) == (0, 0) and not lora and ep & 1 and not ep & 32:
         # the persistent forward kernel (gemm.hip launch256p), one instantiation per epilogue
         # mode (0 plain, 1 bias/residual, 2 activation); one block per CU
-        return "gemm256p_k<MODE>", min(int(g.value), 256)  # 256 CUs on MI355X
+        return ("gemm256pd_k<MODE>" if direct else "gemm256p_k<MODE>"), min(int(g.value), 256)  # 256 CUs on MI355X
     if tile >= 100:  # the M-tail split: the head rows' kernel (+ a thin split-K product for the rest)
         return names.get(tile - 100, f"tile{tile - 100}<{al}, {bl}>") + " M-split", int(g.value)
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)

@@ -16,16 +16,25 @@ which bench.py reads for the same (workload, kernel) pair only.
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 
 
+def name_pattern(kname):
+    """kname as a regex: "<MODE>" matches every epilogue-mode instantiation of a kernel, "*" one
+    integer template argument (bench.gemm_kernel_name's EPI wildcard)"""
+    pat = re.escape(kname).replace(re.escape("<MODE>"), r"<\d+>").replace(re.escape("*"), r"\d+")
+    return re.compile(pat)
+
+
 def per_dispatch(path, kname):
     """counters per dispatch of the kernel whose name (template arguments as rocprofv3 prints
-    them) contains kname; "<MODE>" matches every epilogue-mode instantiation of a kernel"""
+    them) matches kname (name_pattern)"""
     d = defaultdict(dict)
+    pat = name_pattern(kname)
     for r in csv.DictReader(open(path)):
-        if kname.replace("<MODE>", "<") in r["Kernel_Name"]:
+        if pat.search(r["Kernel_Name"]):
             key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(d))
             d[key][r["Counter_Name"]] = d[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return d
