@@ -420,18 +420,23 @@ DEV unsigned dma_base0(int64_t ld, int64_t idx0, int lw, int lane) {
   return (unsigned)(((idx0 + row) * ld + chunk * 8) * 2);
 }
 
+template <int NP = 8>
 DEV void dma_issue_stride(__amdgpu_buffer_rsrc_t rsrc, unsigned base, unsigned step, int soff, char* lds, int lw) {
   unsigned off = base;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < NP; ++i) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds + (lw + 4 * i) * 1024), 16, off, soff, 0, 0);
     off += step;
     asm volatile("" : "+v"(off));  // no precomputed per-piece offsets live across the K-loop
   }
 }
 
-template <int MODE>
+// BMT: 256 or 288 rows (the 288-row tile of the N = 4096 / long-K forward products: 36 A pieces, nine
+// per loader wave)
+template <int MODE, int BMT>
 __global__ __launch_bounds__(512, 1) void gemm256pd_k(GemmArgs p) {
+  constexpr int TMW = BMT / 32, NPA = BMT / 32;  // MFMA rows per wave; A pieces per loader wave
+  constexpr int TA = BMT * BK * 2, STAGE = TA + 256 * BK * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -447,62 +452,67 @@ __global__ __launch_bounds__(512, 1) void gemm256pd_k(GemmArgs p) {
   const __amdgpu_buffer_rsrc_t rc = make_rsrc((const u16*)p.C, ((p.M - 1) * p.ldc + p.N) * 2);
   const unsigned step_a = (unsigned)(32 * p.lda * 2), step_b = (unsigned)(32 * p.ldb * 2);
   PTile xy = ptile(p, xcd_remap(t, p.sk_dp));
-  int64_t m0 = (int64_t)xy.tm * 256, n0 = (int64_t)xy.tn * 256;
+  int64_t m0 = (int64_t)xy.tm * BMT, n0 = (int64_t)xy.tn * 256;
   if (loader) {
-    dma_issue_stride(ra, dma_base0(p.lda, m0, lw, lane), step_a, 0, smem, lw);
-    dma_issue_stride(rb, dma_base0(p.ldb, n0, lw, lane), step_b, 0, smem + P_TA, lw);
+    dma_issue_stride<NPA>(ra, dma_base0(p.lda, m0, lw, lane), step_a, 0, smem, lw);
+    dma_issue_stride(rb, dma_base0(p.ldb, n0, lw, lane), step_b, 0, smem + TA, lw);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   praw_barrier();
   int s = 0;
   bool k1_early = false;  // this tile's K-tile 1 went out before the previous tile's stores
-  f32x4 acc[8][4];
+  f32x4 acc[TMW][4];
   for (;;) {
     const int t1 = t + (int)gridDim.x;
     const bool has_next = t1 < tiles;
     const PTile xy1 = ptile(p, xcd_remap(has_next ? t1 : t, p.sk_dp));
-    const int64_t m1 = (int64_t)xy1.tm * 256, n1 = (int64_t)xy1.tn * 256;
+    const int64_t m1 = (int64_t)xy1.tm * BMT, n1 = (int64_t)xy1.tn * 256;
     unsigned ba = dma_base0(p.lda, m0, lw, lane), bb = dma_base0(p.ldb, n0, lw, lane);
     asm volatile("" : "+v"(ba), "+v"(bb));
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < TMW; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt) {
-      char* cur = smem + ((s + kt) & 1) * P_STAGE;
-      char* nxt = smem + ((s + kt + 1) & 1) * P_STAGE;
+      char* cur = smem + ((s + kt) & 1) * STAGE;
+      char* nxt = smem + ((s + kt + 1) & 1) * STAGE;
       if (loader && !(kt == 0 && k1_early)) {
         if (kt + 1 < nk) {
           const int64_t k1 = (int64_t)(kt + 1) * BK;
-          dma_issue_stride(ra, ba, step_a, dma_soff<0>(k1, p.lda), nxt, lw);
-          dma_issue_stride(rb, bb, step_b, dma_soff<0>(k1, p.ldb), nxt + P_TA, lw);
+          dma_issue_stride<NPA>(ra, ba, step_a, dma_soff<0>(k1, p.lda), nxt, lw);
+          dma_issue_stride(rb, bb, step_b, dma_soff<0>(k1, p.ldb), nxt + TA, lw);
         } else if (has_next) {  // the next tile's first K-tile under this tile's last MFMAs
           unsigned b1a = dma_base0(p.lda, m1, lw, lane), b1b = dma_base0(p.ldb, n1, lw, lane);
           asm volatile("" : "+v"(b1a), "+v"(b1b));
-          dma_issue_stride(ra, b1a, step_a, 0, nxt, lw);
-          dma_issue_stride(rb, b1b, step_b, 0, nxt + P_TA, lw);
+          dma_issue_stride<NPA>(ra, b1a, step_a, 0, nxt, lw);
+          dma_issue_stride(rb, b1b, step_b, 0, nxt + TA, lw);
         }
       }
-      tile_mfma<0, 0, 256, 256, 8, 4>(cur, wm, wn, lane, acc);
-      // loaders: K-tile 0 after an early K-tile 1 leaves the previous tile's 16 stores (issued after
-      // that DMA) in flight; otherwise everything the wave issued has landed. The other waves issue
-      // no vector-memory op in the K-loop: they never wait, so their epilogue stores drain under it
+      tile_mfma<0, 0, BMT, 256, TMW, 4>(cur, wm, wn, lane, acc);
+      // loaders: K-tile 0 after an early K-tile 1 leaves the previous tile's 2 TMW stores (issued
+      // after that DMA) in flight; otherwise everything the wave issued has landed. The other waves
+      // issue no vector-memory op in the K-loop: they never wait, so their epilogue stores drain
+      // under it
       if (loader) {
-        if (kt == 0 && k1_early) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (kt == 0 && k1_early) {
+          if constexpr (TMW == 9) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
       praw_barrier();
     }
     // every wave is past the last K-tile's barrier: its stage is free for the next tile's K-tile 1
     k1_early = has_next && nk > 1;
     if (k1_early && loader) {
-      char* st1 = smem + ((s + nk + 1) & 1) * P_STAGE;
+      char* st1 = smem + ((s + nk + 1) & 1) * STAGE;
       unsigned b1a = dma_base0(p.lda, m1, lw, lane), b1b = dma_base0(p.ldb, n1, lw, lane);
       asm volatile("" : "+v"(b1a), "+v"(b1b));
-      dma_issue_stride(ra, b1a, step_a, dma_soff<0>(BK, p.lda), st1, lw);
-      dma_issue_stride(rb, b1b, step_b, dma_soff<0>(BK, p.ldb), st1 + P_TA, lw);
+      dma_issue_stride<NPA>(ra, b1a, step_a, dma_soff<0>(BK, p.lda), st1, lw);
+      dma_issue_stride(rb, b1b, step_b, dma_soff<0>(BK, p.ldb), st1 + TA, lw);
     }
-    direct_epilogue<MODE, 8>(p, acc, rc, m0 + wm * 128, n0 + wn * 64, lane);
+    direct_epilogue<MODE, TMW>(p, acc, rc, m0 + wm * (BMT / 2), n0 + wn * 64, lane);
     if (!has_next) break;
     s = (s + nk) & 1;
     t = t1;
@@ -529,19 +539,20 @@ int launch256p_m(GemmArgs p, hipStream_t s) {
   return cullavo_check_launch("gemm256 persistent");
 }
 
-template <int MODE>
+template <int MODE, int BMT = 256>
 int launch256pd_m(GemmArgs p, hipStream_t s) {
-  const int smem = 2 * P_STAGE;
+  const int smem = 2 * (BMT * BK * 2 + 256 * BK * 2);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256pd_k<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)gemm256pd_k<MODE, BMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
     attr_set = true;
   }
-  p.tiles_m = (int)cdiv(p.M, 256);
+  p.tiles_m = (int)cdiv(p.M, BMT);
   p.tiles_n = (int)cdiv(p.N, 256);
   p.sk_dp = p.tiles_m * p.tiles_n;
   const int grid = std::min(p.sk_dp, num_cus());
-  gemm256pd_k<MODE><<<(unsigned)grid, 512, smem, s>>>(p);
+  gemm256pd_k<MODE, BMT><<<(unsigned)grid, 512, smem, s>>>(p);
   return cullavo_check_launch("gemm256 persistent direct");
 }
 
@@ -560,6 +571,17 @@ int lean_mode(const GemmArgs& p) {
 
 // C addressable by one buffer descriptor (the direct epilogue's stores)
 bool c_fits_rsrc(const GemmArgs& p) { return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB; }
+
+// the persistent 288-row direct kernel for a lean (0,0) product (the 7B forward products the plan puts
+// on 288-row tiles); -1: not eligible
+int launch288pd(const GemmArgs& p, hipStream_t s) {
+  if (p.part != nullptr || !p.epi_lds || (p.epi_lds & (128 | 32)) || !p.dma_pre || !c_fits_rsrc(p)) return -1;
+  const int mode = lean_mode(p);
+  if (mode == 0) return launch256pd_m<0, 288>(p, s);
+  if (mode == 1) return launch256pd_m<1, 288>(p, s);
+  if (mode == 2) return launch256pd_m<2, 288>(p, s);
+  return -1;
+}
 
 // the persistent kernel for the lean epilogue cases (plain, bias / residual, activation); -1: none.
 // cullavo_gemm_set_epilogue bit 7 keeps the LDS-staged epilogue (gemm256p_k) for A/B
@@ -1006,6 +1028,10 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
                          : launch256<0, 1, CULLAVO_DT_BF16, 256, 256, false, true>(p, s);
   }
   if (tile == kT288x256) {  // a_layout 0 (above), one loader wave per SIMD
+    if (!f32 && b_layout == 0 && g_persist) {
+      const int rc = launch288pd(p, s);
+      if (rc != -1) return rc;
+    }
     if (!f32) {
       const int rc = b_layout == 0 ? launch256_lean<0, 0, 288>(p, s) : launch256_lean<0, 1, 288>(p, s);
       if (rc != -1) return rc;

@@ -18,7 +18,8 @@ Attention (config-3 head shape D = 128 causal at L = 1088, ViT D = 64 non-causal
   rel-L2 3e-3 of the f64 reference (measured 2.0-2.5e-3: the FA2 arithmetic rounds P and dS to bf16
   once per element, ~1.1e-3 each, plus the output's own bf16 rounding ~1.1e-3) and element-wise
   within 2^-3 of (|ref| + rms of ref's row) (one head's D values of one token; + 1e-3 of the
-  tensor's rms for rows whose exact value is 0): a dropped or
+  tensor's rms for rows whose exact value is 0; the reference's delta = rowsum(dO * O) uses the
+  forward's stored O, as FA2 does): a dropped or
   double-counted key / query tile moves the rows it touches by ~0.3 of their size and fails it.
 The f64 references run on the GPU (torch), the checked kernels through the C-ABI (ops.*). Stats of
 every case are appended to gpurun_out/accuracy_stats.jsonl on the box.
@@ -98,8 +99,11 @@ def test_gemm_f32_accumulation_and_bf16_bitwise(name, M, N, K, al, bl):
     assert ndiff == 0, f"{name}: {ndiff} bf16 outputs differ from bf16(f32 output of the same product)"
 
 
-def _attn_ref(q, k, v, do, B, H, L, D, scale, causal):
-    """f64 attention forward + backward of [B*L, H*D] row-major q, k, v, dO"""
+def _attn_ref(q, k, v, do, B, H, L, D, scale, causal, o_kernel):
+    """f64 attention forward + backward of [B*L, H*D] row-major q, k, v, dO. The backward's
+    delta = rowsum(dO * O) takes the forward's output as stored (o_kernel, bf16), as FA2 defines it:
+    with the exact O instead, rows with few live keys (the causal diagonal's first queries) differ by
+    the cancellation in dP - delta, not by anything the backward kernels compute."""
     def heads(x):
         return x.double().view(B, L, H, D).transpose(1, 2)  # [B, H, L, D]
     Q, Kt, V, dO = heads(q), heads(k), heads(v), heads(do)
@@ -111,7 +115,7 @@ def _attn_ref(q, k, v, do, B, H, L, D, scale, causal):
     O = P @ V
     dV = P.transpose(-1, -2) @ dO
     dP = dO @ V.transpose(-1, -2)
-    delta = (dO * O).sum(-1, keepdim=True)
+    delta = (dO * heads(o_kernel)).sum(-1, keepdim=True)
     dS = P * (dP - delta)
     dQ = dS @ Kt * scale
     dK = dS.transpose(-1, -2) @ Q * scale
@@ -133,7 +137,7 @@ def test_attention_against_f64(name, B, H, L, D, causal):
     o, lse = ops().attn_fwd(q, k, v, B=B, H=H, Lq=L, Lk=L, D=D, scale=scale, causal=causal)
     dq, dk, dv = ops().attn_bwd(q, k, v, o, do, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=scale, causal=causal)
     torch.cuda.synchronize()
-    O, LSE, dQ, dK, dV = _attn_ref(q, k, v, do, B, H, L, D, scale, causal)
+    O, LSE, dQ, dK, dV = _attn_ref(q, k, v, do, B, H, L, D, scale, causal, o)
     rec = {"test": "attention", "case": name, "B": B, "H": H, "L": L, "D": D, "causal": causal}
     lse_err = (lse.double() - LSE).abs().max().item()
     rec["lse_max_abs"] = lse_err

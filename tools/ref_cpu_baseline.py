@@ -56,19 +56,20 @@ def timed_step(n_lm: int, n_vit: int, dtype: torch.dtype, reps: int) -> float:
         out.loss.backward()
 
     step()  # warm
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         step()
-    dt = (time.perf_counter() - t0) / reps
+        ts.append(time.perf_counter() - t0)
     del model
-    return dt
+    return sorted(ts)[len(ts) // 2]  # median
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     ap.add_argument("--dtype", default="both", choices=["fp32", "bf16", "both"])
-    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     out = {"what": "reference CuLLaVOModel.forward + backward (vision frozen), one config-3 sample "
