@@ -531,12 +531,17 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
     names = {0: f"gemm_k<{al}, {bl}, 1, 0>", 2: g256(256), 3: g256(192),
              9: f"gemm256_k<{al}, {bl}, 1, 256, 256, 1, false, false, 0> split-K + splitk_reduce_k<1>",
              10: g256(288), 14: "gemv_k<1, 0, 1, 0, 4>" if K >= 8192 else ("gemv_k<1, 0, 1, 0, 4, 16>" if N > 16384 else "gemv_k<1, 0, 1, 0, 8>")}
-    if tile == 2 and (al, bl) == (0, 0) and not lora and ep & 1 and not ep & 32:
-        # the persistent forward kernel (gemm.hip launch256p), one instantiation per epilogue
-        # mode (0 plain, 1 bias/residual, 2 activation); one block per CU
-        return ("gemm256pd_k<MODE>" if direct else "gemm256p_k<MODE>"), min(int(g.value), 256)  # 256 CUs on MI355X
+    def persistent(t):
+        # the persistent forward kernels (gemm.hip launch256p / launch288pd), one instantiation per
+        # epilogue mode (0 plain, 1 bias/residual, 2 activation); one block per CU
+        if t in (2, 10) and (al, bl) == (0, 0) and not lora and ep & 1 and not ep & 32 and (t == 2 or direct):
+            return f"gemm256pd_k<*, {256 if t == 2 else 288}>" if direct else "gemm256p_k<MODE>"
+        return None
     if tile >= 100:  # the M-tail split: the head rows' kernel (+ a thin split-K product for the rest)
-        return names.get(tile - 100, f"tile{tile - 100}<{al}, {bl}>") + " M-split", int(g.value)
+        base = persistent(tile - 100) or names.get(tile - 100, f"tile{tile - 100}<{al}, {bl}>")
+        return base + " M-split", int(g.value)
+    if persistent(tile):
+        return persistent(tile), min(int(g.value), 256)  # 256 CUs on MI355X
     return names.get(tile, f"tile{tile}<{al}, {bl}>"), int(g.value)
 
 

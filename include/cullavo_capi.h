@@ -181,7 +181,11 @@ int cullavo_gemm_set_splitk_target(int blocks);
    and store 16-B groups of 8 columns; 0 = per-lane 8-B stores straight from the MFMA layout.
    Bit 1: C is written with non-temporal (streaming) stores. Bits 2 / 3 / 4 (round 5, A/B): send
    the LDS epilogue's lean bias/residual, plain-output and activation / SwiGLU-backward paths to
-   the general per-option path (same values). Returns the previous setting. */
+   the general per-option path (same values). Bit 5: no persistent forward kernel. Round 6, A/B
+   (same values): bit 6 keeps the SwiGLU-backward dX on the general epilogue path instead of its
+   prefetching instantiation; bit 7 keeps the LDS-staged epilogue for the lean cases instead of
+   the direct (register, 16-B buffer store) epilogue and its persistent forward kernels.
+   Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets
    computed once per tile and the K advance passed as the scalar offset (used when K % 64 == 0

@@ -6,7 +6,7 @@ TAG=${1:-prof}
 bash tools/profile_round.sh $TAG/config3-full config3-full "gemm256_k<1, 1, 1, 256, 256, 1, false, false, 1>"
 bash tools/profile_round.sh $TAG/config3-lora config3-lora "gemm256_k<0, 0, 1, 288, 256, 1, true, false, 0>" --trainable lora
 bash tools/profile_round.sh $TAG/config5-full config5-full "gemm256_k<1, 1, 1, 256, 256, 1, false, false, 1>" --config llava-1.5-13b --batch 4 --text-len 1025
-bash tools/profile_round.sh $TAG/config2-vit config2-vit "gemm256pd_k<MODE>" --workload vit --batch 64
+bash tools/profile_round.sh $TAG/config2-vit config2-vit "gemm256pd_k<*, 256>" --workload vit --batch 64
 python - "$TAG" <<'PY'
 import json, sys
 tag = sys.argv[1]
