@@ -573,8 +573,11 @@ int lean_mode(const GemmArgs& p) {
 bool c_fits_rsrc(const GemmArgs& p) { return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB; }
 
 // the persistent 288-row direct kernel for a lean (0,0) product (the 7B forward products the plan puts
-// on 288-row tiles); -1: not eligible
+// on 288-row tiles); -1: not eligible. Opt-in (cullavo_gemm_set_epilogue bit 8): on one box
+// (tools/epi_ab.py, profiles/r06/gemm/epi_ab.txt) it beat the data-parallel 288-row direct kernel on
+// gate|up (1349 vs 1340 TF/s) but lost on q|k|v, o and down (1358 / 1284 / 1305 vs 1390 / 1317 / 1314)
 int launch288pd(const GemmArgs& p, hipStream_t s) {
+  if (!(p.epi_lds & 256)) return -1;
   if (p.part != nullptr || !p.epi_lds || (p.epi_lds & (128 | 32)) || !p.dma_pre || !c_fits_rsrc(p)) return -1;
   const int mode = lean_mode(p);
   if (mode == 0) return launch256pd_m<0, 288>(p, s);
@@ -832,11 +835,12 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 252);
-  g_epi_lds = lds_staged & 253;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 508);
+  g_epi_lds = lds_staged & 509;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
                                  // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel;
                                  // bit 6 the prefetching SwiGLU-backward instantiation; bit 7 the direct
-                                 // (register) epilogue of the lean cases
+                                 // (register) epilogue of the lean cases; bit 8 the persistent 288-row
+                                 // direct forward kernel (opt-in)
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }
@@ -1053,8 +1057,8 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
       const int rc = launch256p(p, s);
       if (rc != -1) return rc;
     }
-    if (!f32 && a_layout == 0 && b_layout == 1) {
-      const int rc = launch256_lean<0, 1, 256>(p, s);
+    if (!f32 && a_layout == 0) {
+      const int rc = b_layout == 1 ? launch256_lean<0, 1, 256>(p, s) : launch256_lean<0, 0, 256>(p, s);
       if (rc != -1) return rc;
     }
     if (!f32 && a_layout == 1 && b_layout == 1) {

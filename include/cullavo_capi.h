@@ -184,7 +184,8 @@ int cullavo_gemm_set_splitk_target(int blocks);
    the general per-option path (same values). Bit 5: no persistent forward kernel. Round 6, A/B
    (same values): bit 6 keeps the SwiGLU-backward dX on the general epilogue path instead of its
    prefetching instantiation; bit 7 keeps the LDS-staged epilogue for the lean cases instead of
-   the direct (register, 16-B buffer store) epilogue and its persistent forward kernels.
+   the direct (register, 16-B buffer store) epilogue and its persistent forward kernel; bit 8 opts
+   into the persistent 288-row direct forward kernel.
    Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets

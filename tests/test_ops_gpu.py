@@ -177,7 +177,7 @@ def test_gemm_direct_epilogue_bitwise(M, N, K, al, bl, tile, epi):
     prev_t, prev_e = L.cullavo_gemm_set_tile(tile), L.cullavo_gemm_set_epilogue(1)
     outs = []
     try:
-        for mode in (1, 1 | 128, 0):
+        for mode in (1, 1 | 128, 0, 1 | 256):  # default, LDS-staged, per-lane, persistent 288-row opt-in
             L.cullavo_gemm_set_epilogue(mode)
             C = torch.full((M, N), float("nan"), dtype=BF, device=DEV)
             ops().gemm(al, bl, M, N, K, A, A.stride(0), B, B.stride(0), C, N, bias=bias, act=act, residual=res,
@@ -197,6 +197,7 @@ def test_gemm_direct_epilogue_bitwise(M, N, K, al, bl, tile, epi):
     close(outs[0], ref, 8e-3, f"direct epilogue {epi}")
     assert torch.equal(outs[0], outs[1]), "direct vs LDS-staged epilogue"
     assert torch.equal(outs[0], outs[2]), "direct vs per-lane epilogue"
+    assert torch.equal(outs[0], outs[3]), "direct vs the persistent 288-row direct kernel (opt-in)"
 
 
 @pytest.mark.parametrize("M,N,K,al,bl", [(2304, 8192, 1024, 0, 0), (1032, 2056, 4104, 1, 1), (2000, 1544, 520, 0, 1),

@@ -6,8 +6,8 @@ fine-tune's trainable set (vision frozen: no vision gradients are requested, as 
 
 The whole 7B model does not fit this 64 GiB container in fp32 with gradients, so the per-sample
 time is assembled from the reference's own code at reduced depth: the same model with 1 and with 2
-decoder layers (their difference is one decoder layer's forward + backward) and with 2 and 3 CLIP
-layers (hidden_states[-2] runs 1 and 2 of them: one CLIP layer's forward), then
+decoder layers (their difference is one decoder layer's forward + backward), and the vision tower's
+own forward (no autograd: the tower is frozen) with 2 and 3 CLIP layers (one CLIP layer), then
   t_sample = t(1 LM, 2 ViT) + 31 x d_LM + 22 x d_ViT   (32 LM layers, the 23 ViT layers the step runs).
 Run here, in the build container (the reference is not on the GPU box): writes the record to
 profiles/r06/ref_cpu_baseline.json. bench.py's cpu_baseline (kind "port") is the oracle timed on the
@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 from oracle import cullavo_oracle as O  # noqa: E402
 
 
-def timed_step(n_lm: int, n_vit: int, dtype: torch.dtype, reps: int) -> float:
+def timed_step(n_lm: int, n_vit: int, dtype: torch.dtype, reps: int, vit_only: bool = False) -> float:
     import make_golden as MG  # the reference shim (imports /root/reference)
     cfg = O.config_7b()
     cfg.text.num_hidden_layers = n_lm
@@ -55,11 +55,16 @@ def timed_step(n_lm: int, n_vit: int, dtype: torch.dtype, reps: int) -> float:
         out = model(input_ids=ids, pixel_values=pix, attention_mask=mask, labels=labels, return_dict=True)
         out.loss.backward()
 
-    step()  # warm
+    def vit():  # the reference's vision call (arch_cullavo.py:586-597), frozen: no autograd
+        with torch.no_grad():
+            model.vision_tower(pix, output_hidden_states=True)
+
+    fn = vit if vit_only else step
+    fn()  # warm
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        step()
+        fn()
         ts.append(time.perf_counter() - t0)
     del model
     return sorted(ts)[len(ts) // 2]  # median
@@ -85,8 +90,9 @@ def main():
         name = "fp32" if dt == torch.float32 else "bf16"
         t11 = timed_step(1, 2, dt, a.reps)
         t21 = timed_step(2, 2, dt, a.reps)
-        t12 = timed_step(1, 3, dt, a.reps)
-        d_lm, d_vit = t21 - t11, t12 - t11
+        # one CLIP layer from the vision tower's own forward at 2 and 3 layers (5 reps: it is short)
+        d_vit = timed_step(1, 3, dt, 5, vit_only=True) - timed_step(1, 2, dt, 5, vit_only=True)
+        d_lm = t21 - t11
         sample = t11 + 31 * d_lm + 22 * d_vit
         out["results"][name] = {"t_1lm_1vit_s": round(t11, 3), "lm_layer_fwd_bwd_s": round(d_lm, 3),
                                 "vit_layer_fwd_s": round(d_vit, 3), "sample_s": round(sample, 2),
