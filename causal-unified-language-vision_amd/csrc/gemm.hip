@@ -747,6 +747,21 @@ int g_msplit = 1;
 // fc2 (K = 4096: 3 -> 2 rounds of 288-row tiles), not fc1 / o (K = 1024)
 double rem_seconds(int64_t rows, int64_t N, int64_t K) { return 2.0 * rows * N * K / 150e12 + 16e-6; }
 
+// a round split's tail (round 6): when its 256x256 grid fits half the CUs and K is long, the tail rows
+// run split over K on the 8-wave kernel (splitk256_plan): its rounds at K / s plus the f32 partials'
+// write + reduce; otherwise the thin product of rem_seconds
+double tail_seconds(int64_t rows, int64_t N, int64_t K) {
+  int per = 0;
+  const int s = splitk256_plan(rows, N, K, &per);
+  if (s > 1) {
+    const int64_t tiles = cdiv(rows, 256) * cdiv(N, 256);
+    const double t_tile = 2.0 * 256 * 256 * (double)per * BK * 256 / (g_tile_rate[0] * 1e12);
+    const double reduce = (double)rows * N * 4 * s * 2 / 5e12 + 10e-6;
+    return (double)cdiv(tiles * s, num_cus()) * t_tile + reduce;
+  }
+  return rem_seconds(rows, N, K);
+}
+
 int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_t* m_main = nullptr) {
   if (m_main) *m_main = 0;
   if (force >= 0) return force;
@@ -776,6 +791,21 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_
     if (m_main && g_msplit && c.id != kT128 && mm > 0 && M - mm > 16) {
       const double ts = seconds(c, mm) + rem_seconds(M - mm, N, K);
       if (ts < best_split * 0.999) { best_split = ts; bid_split = c.id; mm_split = mm; }
+    }
+    // round split (round 6): when the N-tiles divide the CU slots, the head as whole rounds of tiles
+    // and the last partial round's rows as a product of their own, split over K on the 8-wave kernel
+    // (tail_seconds): the gate|up weight gradient 22016 x 4096 x 8704 is 5.375 rounds of 256x256
+    // tiles -> 5 rounds + 96 tiles at half K
+    if (m_main && g_msplit && c.id != kT128) {
+      const int64_t tn = cdiv(N, c.bn);
+      if (c.slots % tn == 0) {
+        const int64_t mpr = c.slots / tn, full = cdiv(M, c.bm) / mpr;
+        const int64_t mm2 = full * mpr * c.bm;
+        if (full >= 1 && mm2 < M && M - mm2 > 16 && mm2 != mm) {
+          const double ts = seconds(c, mm2) + tail_seconds(M - mm2, N, K);
+          if (ts < best_split * 0.999) { best_split = ts; bid_split = c.id; mm_split = mm2; }
+        }
+      }
     }
   }
   if (m_main && best_split < 0.95 * best) {

@@ -126,6 +126,34 @@ def test_gemm_msplit(M, N, K, act):
     close(y[:mm][::97], y_tile[:mm][::97], 0.0, "head rows")
 
 
+def test_gemm_round_split_weight_gradient():
+    """The round split (round 6; cullavo_gemm_plan 100 + tile with the head on whole rounds): the
+    gate|up weight gradient 22016 x 4096 x 8704 is 5.375 rounds of 256x256 tiles, so the plan runs
+    5 rounds (20480 rows) on the 8-wave kernel and the last 1536 rows split over K on the same
+    kernel (f32 partials reduced in split order). Head rows are bitwise the unsplit product's,
+    tail rows match the fp32 product."""
+    from cullavo_amd import _lib
+    L = _lib.lib()
+    T, Fo, d = 8704, 22016, 4096
+    plan = L.cullavo_gemm_plan(Fo, d, T, 1, 1, None)
+    assert plan == 102, plan
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dy = torch.randn(T, Fo, device=DEV, generator=g).to(BF)
+    x = torch.randn(T, d, device=DEV, generator=g).to(BF)
+    dw = torch.empty(Fo, d, dtype=BF, device=DEV)
+    ops().linear_dw(dy, x, dw)
+    prev = L.cullavo_gemm_set_tile(2)
+    try:
+        dw_whole = torch.empty(Fo, d, dtype=BF, device=DEV)
+        ops().linear_dw(dy, x, dw_whole)
+    finally:
+        L.cullavo_gemm_set_tile(prev)
+    mm = 20480
+    assert torch.equal(dw[:mm], dw_whole[:mm])
+    ref = dy[:, mm:].float().T @ x.float()  # dW rows = dy columns
+    close(dw[mm:], ref, 8e-3, "round-split tail rows")
+
+
 @pytest.mark.parametrize("act", ["gelu", "quick_gelu"])
 def test_gemm_epilogue_paths_bit_identical(tile_mode, act):
     """The LDS-staged 16-B epilogue (packed quick_gelu) and the per-lane one compute the same
