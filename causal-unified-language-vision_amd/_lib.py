@@ -115,6 +115,8 @@ def lib():
             L.cullavo_gemm_set_epilogue(int(os.environ["CULLAVO_GEMM_EPILOGUE"]))
         if os.environ.get("CULLAVO_GEMM_DMA"):  # DMA-offset A/B (cullavo_gemm_set_dma)
             L.cullavo_gemm_set_dma(int(os.environ["CULLAVO_GEMM_DMA"]))
+        if os.environ.get("CULLAVO_GEMV_NT"):  # decode weight-load policy A/B (cullavo_gemv_set_nt)
+            L.cullavo_gemv_set_nt(int(os.environ["CULLAVO_GEMV_NT"]))
         if os.environ.get("CULLAVO_RATE288") is not None:  # 288-row tile A/B (0 = out of the plan)
             L.cullavo_gemm_set_tile_rate(10, float(os.environ["CULLAVO_RATE288"]), None)
         if os.environ.get("CULLAVO_ATTN_RESCALE"):  # deferred-rescale A/B (cullavo_attn_set_rescale)

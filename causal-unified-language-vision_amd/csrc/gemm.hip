@@ -742,6 +742,8 @@ double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 // on that tile and the remaining rows as a second, thin product (128x128 tiles, split over K
 // when the caller gives the workspace), if that is estimated at least 5 % faster.
 int g_msplit = 1;
+// 288-row tiles at K < 2048 (cullavo_gemm_set_epilogue bit 9, A/B; off: the round-3 exclusion below)
+int g_short288 = 0;
 // the thin product's time: its split-K launch + reduce cost 16-19 us at the ViT shapes (64 rows:
 // profiles/r05/vit/vit_kernel_trace.txt), so a split pays only where it saves more than that --
 // fc2 (K = 4096: 3 -> 2 rounds of 288-row tiles), not fc1 / o (K = 1024)
@@ -781,7 +783,7 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_
     // 288 rows only for long K: with 16 K-tiles (the ViT's K = 1024 products) its larger
     // per-tile prologue and 144 KiB epilogue cost more than the rounds it saves (config 2:
     // fc1 36928x4096x1024 at 815 TF/s against 865 for the 256-row tile)
-    if (c.id == kT288x256 && K < 2048) continue;
+    if (c.id == kT288x256 && K < 2048 && !g_short288) continue;
     if (c.rate <= 0.0) continue;
     const double t = seconds(c, M);
     if (t < best * 0.999) { best = t; bid = c.id; }
@@ -865,12 +867,13 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 508);
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 508) | (g_short288 << 9);
   g_epi_lds = lds_staged & 509;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
                                  // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel;
                                  // bit 6 the prefetching SwiGLU-backward instantiation; bit 7 the direct
                                  // (register) epilogue of the lean cases; bit 8 the persistent 288-row
                                  // direct forward kernel (opt-in)
+  g_short288 = (lds_staged >> 9) & 1;  // bit 9: 288-row tiles at K < 2048 (A/B)
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }

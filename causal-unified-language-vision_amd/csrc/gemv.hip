@@ -70,7 +70,8 @@ DEV frag8 gemv_xfrag(const GemvArgs& a, const u16* xp, int64_t off, int64_t k, c
 // g and u of one output: y = bf16(bf16(silu(g)) * u) with g, u first rounded to bf16 as the
 // unfused product stores them -- bitwise swiglu_fwd_k of that product, without its launch or the
 // [M, 2N] round trip.
-template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves, int OT = 0>
+// WNT: the weight fragments by non-temporal loads (read once per step; cullavo_gemv_set_nt)
+template <int CT, int ORDER, int RB, int XF, int NBW = kGemvBatch, int NW = kGemvWaves, int OT = 0, bool WNT = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 16 ? 2 : (NBW >= 8 || XF == 1) ? 4 : 8))) void gemv_k(GemvArgs a) {
   static_assert(OT == 0 || RB == 1, "SwiGLU pairing: one 16-row block per workgroup");
   const GemmArgs& p = a.g;
@@ -132,7 +133,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
       const int64_t off = in ? ks * 32 : 0;
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
-        w[i][rb] = in ? __builtin_bit_cast(frag8, *reinterpret_cast<const u16x8*>(wrow[rb] + off)) : frag8{};
+        w[i][rb] = in ? __builtin_bit_cast(frag8, WNT ? __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wrow[rb] + off))
+                                                      : *reinterpret_cast<const u16x8*>(wrow[rb] + off))
+                      : frag8{};
     }
     if (XF == 1 && j0 == 0) {
       // RMSNorm of the M rows, after the first batch of weight loads is in flight, by every thread of
@@ -222,7 +225,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NBW >= 
   }
 }
 
+int g_gemv_nt = 0;  // non-temporal weight loads (cullavo_gemv_set_nt)
+
 }  // namespace
+
+// non-temporal weight loads in the decode GEMV on (1) / off (0); returns the previous setting
+extern "C" int cullavo_gemv_set_nt(int on) {
+  const int prev = g_gemv_nt;
+  g_gemv_nt = on & 1;
+  return prev;
+}
 
 int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   // lab switch (CULLAVO_GEMV: 0 contiguous K ranges, 1 round-robin k-steps, 2 / 3 = 0 / 1 with
@@ -239,11 +251,13 @@ int cvgemm_launch_gemv(const cvgemm::GemmArgs& p, bool f32, hipStream_t s) {
   const unsigned grid = (unsigned)cdiv(p.N, 16 * rb);
   GemvArgs a{};
   a.g = p;
-#define GV(O, R, NBW)                                                                                 \
-  if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);                    \
+#define GV(O, R, NBW)                                                                                         \
+  if (f32) gemv_k<CULLAVO_DT_F32, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);                            \
+  else if (g_gemv_nt) gemv_k<CULLAVO_DT_BF16, O, R, 0, NBW, kGemvWaves, 0, true><<<grid, 64 * kGemvWaves, 0, s>>>(a); \
   else gemv_k<CULLAVO_DT_BF16, O, R, 0, NBW><<<grid, 64 * kGemvWaves, 0, s>>>(a);
 #define GV16(NBW)                                                                                     \
   if (f32) gemv_k<CULLAVO_DT_F32, 0, 1, 0, NBW, 16><<<grid, 64 * 16, 0, s>>>(a);                        \
+  else if (g_gemv_nt) gemv_k<CULLAVO_DT_BF16, 0, 1, 0, NBW, 16, 0, true><<<grid, 64 * 16, 0, s>>>(a);   \
   else gemv_k<CULLAVO_DT_BF16, 0, 1, 0, NBW, 16><<<grid, 64 * 16, 0, s>>>(a);
   if (v == 0) { GV(0, 1, 16) } else if (v == 1) { GV(1, 1, 16) } else if (v == 2) { GV(0, 2, 16) }
   else if (v == 3) { GV(1, 2, 16) } else if (v == 4) { GV(0, 1, 8) } else if (v == 5) { GV(1, 1, 8) }
@@ -288,12 +302,15 @@ extern "C" int cullavo_decode_linear(int x_transform, int64_t M, int64_t N, int6
   // products, 4-load batches for K >= 8192, else 8-load batches (SwiGLU output: the 2N-row product)
   const int64_t wrows = ot ? 2 * N : N;
   const int v = K >= 8192 ? 6 : wrows > 16384 ? 8 : kGemvDefault;
-#define DL(XF, OT)                                                                                          \
-  if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16, OT><<<grid, 64 * 16, smem, s>>>(a);                   \
-  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, kGemvWaves, OT><<<grid, 64 * kGemvWaves, smem, s>>>(a); \
-  else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8, kGemvWaves, OT><<<grid, 64 * kGemvWaves, smem, s>>>(a);
+#define DL1(XF, OT, NT)                                                                                           \
+  if (v == 8) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, 16, OT, NT><<<grid, 64 * 16, smem, s>>>(a);                   \
+  else if (v == 6) gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 4, kGemvWaves, OT, NT><<<grid, 64 * kGemvWaves, smem, s>>>(a); \
+  else gemv_k<CULLAVO_DT_BF16, 0, 1, XF, 8, kGemvWaves, OT, NT><<<grid, 64 * kGemvWaves, smem, s>>>(a);
+#define DL(XF, OT) \
+  if (g_gemv_nt) { DL1(XF, OT, true) } else { DL1(XF, OT, false) }
   if (x_transform == 0) { DL(0, 0) } else if (x_transform == 1) { DL(1, 0) } else if (x_transform == 2) { DL(2, 0) }
   else if (x_transform == 3) { DL(0, 1) } else { DL(1, 1) }
 #undef DL
+#undef DL1
   return cullavo_check_launch("decode_linear");
 }

@@ -185,7 +185,8 @@ int cullavo_gemm_set_splitk_target(int blocks);
    (same values): bit 6 keeps the SwiGLU-backward dX on the general epilogue path instead of its
    prefetching instantiation; bit 7 keeps the LDS-staged epilogue for the lean cases instead of
    the direct (register, 16-B buffer store) epilogue and its persistent forward kernel; bit 8 opts
-   into the persistent 288-row direct forward kernel.
+   into the persistent 288-row direct forward kernel; bit 9 lets the plan take 288-row tiles at
+   K < 2048 (A/B).
    Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets
@@ -193,6 +194,10 @@ int cullavo_gemm_set_epilogue(int lds_staged);
    or the operand is stored [K][rows], layout 1; the default); 0 = offsets recomputed per
    K-tile. Same results either way. Returns the previous setting. */
 int cullavo_gemm_set_dma(int precomputed);
+/* Tuning/A-B switch for the decode product (plan 14, cullavo_decode_linear): 1 = the weight
+   fragments are read with non-temporal loads (each weight byte is read once per token step), 0 =
+   default cache policy. Same results either way. Returns the previous setting. */
+int cullavo_gemv_set_nt(int on);
 /* The kernel shape cullavo_gemm will use for this problem (return value, as above) and its
  * number of workgroups (*grid, nullable) — lets profilers match dispatches to GEMM calls.
  * 9 = the 8-wave 256x256 kernel split over K (a grid of at most half the CUs with >= 32

@@ -3,6 +3,7 @@ shapes, interleaved rounds in one process (guide §5.4 rule 24), random bf16 ope
   direct : the default (direct register epilogue, persistent 256 / 288-row forward kernels)
   lds    : bit 7 (the LDS-staged epilogue and the round-5 persistent kernel)
   nopers : bit 5 (no persistent forward kernel; direct epilogue in the data-parallel kernels)
+  short288 : bit 9 (288-row tiles allowed at K < 2048), short288p: bits 9+8 (and the persistent 288)
 Each case runs with the epilogue it has in the step (plain, residual, bias, quick_gelu).
 
   python tools/epi_ab.py [--rounds 5]
@@ -28,7 +29,7 @@ CASES = [  # name, M, N, K, a_layout, b_layout, epilogue
     ("vit_fc1", 36928, 4096, 1024, 0, 0, "qgelu"), ("vit_qkv", 36928, 3072, 1024, 0, 0, "bias"),
     ("vit_o", 36928, 1024, 1024, 0, 0, "bias_res"), ("vit_fc2", 36928, 1024, 4096, 0, 0, "bias_res"),
 ]
-MODES = {"direct": 1, "lds": 1 | 128, "nopers": 1 | 32}
+ALL_MODES = {"direct": 1, "lds": 1 | 128, "nopers": 1 | 32, "short288": 1 | 512, "short288p": 1 | 512 | 256}
 
 
 def main():
@@ -36,7 +37,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cases", default="")
+    ap.add_argument("--modes", default="direct,lds,nopers")
     a = ap.parse_args()
+    MODES = {m: ALL_MODES[m] for m in a.modes.split(",")}
     L = _lib.lib()
     base = L.cullavo_gemm_set_epilogue(1)
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -71,10 +74,12 @@ def main():
                 e.synchronize()
                 res_t[m].append(fl / (s.elapsed_time(e) / a.iters * 1e-3) / 1e12)
         L.cullavo_gemm_set_epilogue(base)
-        same = all(torch.equal(outs["direct"], o) for o in outs.values())
+        same = all(torch.equal(next(iter(outs.values())), o) for o in outs.values())
         line = f"{name:11s} {M}x{N}x{K} ({al},{bl}) {epi:8s}"
-        for m in MODES:
-            line += f" | {m} {statistics.median(res_t[m]):7.1f}"
+        for m, bits in MODES.items():
+            L.cullavo_gemm_set_epilogue(bits)
+            line += f" | {m} [{L.cullavo_gemm_plan(M, N, K, al, bl, None)}] {statistics.median(res_t[m]):7.1f}"
+        L.cullavo_gemm_set_epilogue(base)
         print(line + f" | bitwise {'equal' if same else 'DIFFERENT'}", flush=True)
         del A, B, C, bias, res
 
