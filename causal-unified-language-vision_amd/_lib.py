@@ -103,6 +103,8 @@ def lib():
         # tuning switches for A/B runs (tools, bench): kernel-choice overrides from the env
         if os.environ.get("CULLAVO_ATTN_BWD_MODE"):
             L.cullavo_attn_set_bwd_tiles(int(os.environ["CULLAVO_ATTN_BWD_MODE"]))
+        if os.environ.get("CULLAVO_ATTN_BWD_STAGE"):  # backward staging A/B (cullavo_attn_set_bwd_stage)
+            L.cullavo_attn_set_bwd_stage(int(os.environ["CULLAVO_ATTN_BWD_STAGE"]))
         if os.environ.get("CULLAVO_GEMM_TILE"):
             L.cullavo_gemm_set_tile(int(os.environ["CULLAVO_GEMM_TILE"]))
         if os.environ.get("CULLAVO_SPLITK_TARGET"):  # split-K plan A/B (cullavo_gemm_set_splitk_target)

@@ -105,11 +105,17 @@ __device__ float g_rescale_thr = 8.f;  // forward's deferred-rescale threshold (
 // box, profiles/r04/attn/attn_fwd_ab.txt)
 int g_fwd_stage = -1;
 // backward staging (cullavo_attn_set_bwd_stage): bit 0 = dK/dV Q / dO by LDS-DMA, bit 1 = the
-// dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT). Round 5: with bit 0 the
-// dK/dV kernel reads every fragment by inline asm one step ahead of its MFMAs (no vmcnt(0) in
-// front of the reads, the dS^T stores left in flight at the tile's end): 7B layer backward
-// 467.5 -> 449.7 us, bitwise equal (profiles/r05/attn/attn_bwd_stage_ab.txt), so bit 0 is the
-// default
+// dQ-from-dS kernel's K / dS^T by LDS-DMA (else registers, StageT), bit 2 = the 4-stage LDS-DMA
+// ring dQ kernel attn_bwd_dq_ring_k (D = 128; round 6, takes precedence over bit 1), bit 3 = the
+// blocked dS^T layout (ds_layout). Round 5: with bit 0 the dK/dV kernel reads every fragment by
+// inline asm one step ahead of its MFMAs (no vmcnt(0) in front of the reads, the dS^T stores left
+// in flight at the tile's end): 7B layer backward 467.5 -> 449.7 us, bitwise equal
+// (profiles/r05/attn/attn_bwd_stage_ab.txt), so bit 0 is the default.
+//
+// ds_layout: the mode-7 dS^T workspace [B H][LkP][LqP] bf16 is stored either row-major (key rows of
+// LqP queries: a dQ tile of 64 keys x 128 queries is 64 runs of 256 B, 2 LqP bytes apart) or
+// blocked by 128-query column blocks ([B H][LqP / 128][LkP][128]: the same tile is one contiguous
+// 16 KiB run). Same bytes, same values; the address is bh st_bh + (q / 128) st_blk + key ldst + q % 128
 int g_bwd_stage = 1;
 
 DEV bool buf_ok(int64_t ld, int nrows, int D) { return ((int64_t)nrows * ld + D) * 2 < (int64_t)kOOB; }
@@ -1458,7 +1464,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
     const u16* __restrict__ V, int64_t ldv, const u16* __restrict__ dO, int64_t lddo,
     const float* __restrict__ LSE, const float* __restrict__ DELTA, u16* __restrict__ dK,
     int64_t lddk, u16* __restrict__ dV, int64_t lddv, int H, int Lq, int Lk, float scale,
-    const int32_t* __restrict__ kv_start, u16* __restrict__ dST, int64_t ldst, int64_t st_bh) {
+    const int32_t* __restrict__ kv_start, u16* __restrict__ dST, int64_t ldst, int64_t st_bh, int64_t st_blk) {
   constexpr int QT = 64, KB = 128;
   constexpr int TQ = QT * D * 2;          // bytes of a Q (or dO) tile
   constexpr int TK = KB * D * 2;          // bytes of the K (or V) image
@@ -1636,7 +1642,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
         // dS^T[key][q] (the bf16 operand of dK) for the dQ kernel: registers 8s..8s+3 / 8s+4..8s+7
         // are query rows 16s + 4hf + 0..3 / 16s + 8 + 4hf + 0..3 of this wave's 32
         const u16x8 w = __builtin_bit_cast(u16x8, df);
-        u16* row = dST + ((int64_t)b * H + h) * st_bh + (int64_t)key * ldst + qt * QT + 32 * u + 16 * s + 4 * hf;
+        // (128-query block (qt QT) / 128 at st_blk: ds_layout)
+        u16* row = dST + ((int64_t)b * H + h) * st_bh + (int64_t)((qt * QT) >> 7) * st_blk + (int64_t)key * ldst +
+                   ((qt * QT) & 127) + 32 * u + 16 * s + 4 * hf;
         *reinterpret_cast<u16x4*>(row) = u16x4{w[0], w[1], w[2], w[3]};
         *reinterpret_cast<u16x4*>(row + 8) = u16x4{w[4], w[5], w[6], w[7]};
       }
@@ -1735,7 +1743,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_k(
 // round_up(Lk, 128) rows (keys) of LqP = round_up(Lq, 128) queries (cullavo_attn_bwd_workspace).
 template <int D, bool CAUSAL, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict__ K, int64_t ldk,
-                                                           const u16* __restrict__ dST, int64_t ldst, int64_t st_bh,
+                                                           const u16* __restrict__ dST, int64_t ldst, int64_t st_bh, int64_t st_blk,
                                                            int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
                                                            int Lq, int Lk, float scale,
                                                            const int32_t* __restrict__ kv_start) {
@@ -1753,7 +1761,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
   const int q = qb * QB + wave * 32 + (lane & 31);
   const int kstart = kv_start ? kv_start[b] : 0;
   const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
-  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * QB;
+  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * st_blk;
 
   f32x16 dq[ND];
 #pragma unroll
@@ -1835,6 +1843,151 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_k(const u16* __restrict
     }
     __syncthreads();
   }
+  }
+  if (q < Lq) {
+    u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[dt][rr * 4 + j] * scale);
+        *reinterpret_cast<u16x4*>(dQb + dt * 32 + 8 * rr + 4 * hf) = w;
+      }
+  }
+}
+
+// dQ = scale dS K from the stored dS^T, the LDS-DMA ring form (round 6; cullavo_attn_set_bwd_stage
+// bit 2). attn_bwd_dq_ds_k keeps one 64-key tile in flight per workgroup (two per CU): 32 KiB of
+// dS^T per CU against the ~50 KiB that HBM latency x the per-CU share of its bandwidth asks for,
+// so it streams dS^T at ~3 TB/s (118 us per 7B layer, MFMA busy 0.14). Here one workgroup per CU
+// holds NST = 4 stages of (K tile, dS^T tile) in LDS and keeps NST - 1 tiles in flight by
+// LDS-DMA (counted vmcnt: the DMA pieces are the only vector-memory ops in the loop, 2 kPer per
+// tile and wave), with the fragment reads by inline asm (a builtin LDS read would make the
+// compiler wait for every DMA in flight first) tied by counted lgkmcnt. Same tiles, same MFMA
+// order, same epilogue as attn_bwd_dq_ds_k: bitwise the same dQ.
+// (NST, LAB: tools/lab/dq_lab.hip only -- LAB bit 0 skips the fragment reads and MFMAs, bit 1 the
+// K tiles' DMA: timing floors, not results)
+template <int D, bool CAUSAL, int NST = 4, int LAB = 0>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_ring_k(const u16* __restrict__ K, int64_t ldk,
+                                                             const u16* __restrict__ dST, int64_t ldst, int64_t st_bh, int64_t st_blk,
+                                                             int LkP, u16* __restrict__ dQ, int64_t lddq, int H,
+                                                             int Lq, int Lk, float scale,
+                                                             const int32_t* __restrict__ kv_start) {
+  static_assert(NST >= 2 && NST <= 4, "2 to 4 stages");
+  constexpr int KT = 64, QB = 128;
+  constexpr int TK = KT * D * 2, TS = KT * QB * 2, BUF = TK + TS;
+  constexpr int NS = KT / 16, ND = D / 32;
+  constexpr unsigned KSTEP = 16 * D * 2, SSTEP = 16 * QB * 2;  // 16 rows: the image swizzle's period
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (Lq + QB - 1) / QB;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int qi = lid % nqb, hb = lid / nqb;
+  const int qb = CAUSAL ? (nqb - 1 - qi) : qi;
+  const int h = hb % H, b = hb / H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hf = lane >> 5;
+  const int q = qb * QB + wave * 32 + (lane & 31);
+  const int kstart = kv_start ? kv_start[b] : 0;
+  const u16* Kb = K + (int64_t)b * Lk * ldk + (int64_t)h * D;
+  const u16* Sb = dST + ((int64_t)b * H + h) * st_bh + qb * st_blk;
+
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = f32x16(0.f);
+  int kend = Lk;
+  if (CAUSAL) kend = min(Lk, qb * QB + QB);
+  const int ntiles = (kend + KT - 1) / KT;
+  const int t0 = kstart / KT;
+
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  StageDMA<KT, D, 4> dk_;
+  StageDMA<KT, QB, 4> ds_;
+  dk_.prep(ldk, wu, lane);
+  ds_.prep(ldst, wu, lane);
+  constexpr int kOps = (LAB & 2 ? 0 : StageDMA<KT, D, 4>::kPer) + StageDMA<KT, QB, 4>::kPer;  // DMA pieces per tile and wave
+  auto issue = [&](int t) {
+    char* bK = smem + ((t - t0) % NST) * BUF;
+    if constexpr (!(LAB & 2)) dk_.issue(Kb, ldk, t * KT, Lk, bK, wu);
+    ds_.issue(Sb, ldst, t * KT, LkP, bK + TK, wu);
+  };
+  // per-lane LDS addresses of tr_frag's two halves (16-key step 0; step s adds s KSTEP / SSTEP)
+  const unsigned sbase = lds_addr(smem);
+  unsigned ko[ND][2], so[2];
+  {
+    const int i = lane & 15, qq = i >> 2, p = i & 3, r0 = 4 * hf + qq;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int ch = ((dt * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+      ko[dt][0] = sbase + kv_off<D>(r0, ch) + 8 * (p & 1);
+      ko[dt][1] = sbase + kv_off<D>(r0 + 8, ch) + 8 * (p & 1);
+    }
+    const int ch = ((wave * 32 + 16 * ((lane >> 4) & 1)) >> 3) + (p >> 1);
+    so[0] = sbase + TK + kv_off<QB>(r0, ch) + 8 * (p & 1);
+    so[1] = sbase + TK + kv_off<QB>(r0 + 8, ch) + 8 * (p & 1);
+  }
+  // one 16-key step's fragments: dS^T (B operand) and the ND K^T fragments (A operands)
+  struct Grp {
+    s16x4 bl, bh, kl[ND], kh[ND];
+  };
+  // (ko / so as parameters: clang rejects a generic lambda's implicit capture used in asm operands)
+  auto grp_issue = [](auto s_c, Grp& g, unsigned slot, const unsigned (&ko)[ND][2], const unsigned (&so)[2]) {
+    constexpr unsigned S = decltype(s_c)::value;
+    asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+                 : "=&v"(g.bl), "=&v"(g.bh)
+                 : "v"(so[0] + slot), "v"(so[1] + slot), "n"(S * SSTEP)
+                 : "memory");
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+      asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%4\n\tds_read_b64_tr_b16 %1, %3 offset:%4"
+                   : "=&v"(g.kl[dt]), "=&v"(g.kh[dt])
+                   : "v"(ko[dt][0] + slot), "v"(ko[dt][1] + slot), "n"(S * KSTEP)
+                   : "memory");
+  };
+  auto grp_tie = [](auto cnt_c, Grp& g) {
+    constexpr int CNT = decltype(cnt_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(g.bl), "+v"(g.bh) : "n"(CNT) : "memory");
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) asm volatile("" : "+v"(g.kl[dt]), "+v"(g.kh[dt]));
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto grp_mfma = [&](const Grp& g) {
+    const frag8 bs = tr_join(g.bl, g.bh);
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_join(g.kl[dt], g.kh[dt]), bs, dq[dt], 0, 0, 0);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using CG = std::integral_constant<int, 2 * (ND + 1)>;  // one group's reads
+  static_assert(NS == 4 && 2 * (ND + 1) <= 15, "lgkmcnt counts one group in flight");
+
+  for (int j = 0; j < NST - 1; ++j)
+    if (t0 + j < ntiles) issue(t0 + j);
+  for (int t = t0; t < ntiles; ++t) {
+    // tile t landed: the tiles after it that are already issued may stay in flight
+    const int after = min(NST - 2, ntiles - 1 - t);
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kOps) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kOps) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every wave's pieces of tile t are in, and every wave is done reading the slot refilled next
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NST - 1 < ntiles) issue(t + NST - 1);
+    if constexpr (LAB & 1) continue;
+    const unsigned slot = (unsigned)(((t - t0) % NST) * BUF);
+    Grp ga, gb;
+    grp_issue(std::integral_constant<unsigned, 0>{}, ga, slot, ko, so);
+    grp_issue(std::integral_constant<unsigned, 1>{}, gb, slot, ko, so);
+    grp_tie(CG{}, ga);
+    grp_mfma(ga);
+    grp_issue(std::integral_constant<unsigned, 2>{}, ga, slot, ko, so);
+    grp_tie(CG{}, gb);
+    grp_mfma(gb);
+    grp_issue(std::integral_constant<unsigned, 3>{}, gb, slot, ko, so);
+    grp_tie(CG{}, ga);
+    grp_mfma(ga);
+    grp_tie(C0{}, gb);
+    grp_mfma(gb);
   }
   if (q < Lq) {
     u16* dQb = dQ + ((int64_t)b * Lq + q) * lddq + (int64_t)h * D;
@@ -1943,10 +2096,10 @@ int bwd8_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u16*
   }
   if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, false, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0, 0);
   else
     attn_bwd_dkdv8_k<D, CAUSAL><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0);
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, nullptr, 0, 0, 0);
   attn_bwd_dq_k<D, CAUSAL, 32><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
       q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
@@ -1962,27 +2115,35 @@ int bwd_ds_launch(const u16* q, int64_t ldq, const u16* k, int64_t ldk, const u1
   attn_delta_k<D><<<(unsigned)cdiv(rows * (D / 8), 256), 256, 0, s>>>(o, ldo, dout, lddo, delta, B, H, Lq);
   const int smem_a = std::max(2 * 128 * D * 2 + 2 * (2 * 64 * D * 2 + 2 * 64 * 4), 2 * 4 * 32 * D * 4);
   const int smem_b = 2 * (64 * D * 2 + 64 * 128 * 2);
+  const int smem_r = 4 * (64 * D * 2 + 64 * 128 * 2);  // attn_bwd_dq_ring_k's 4 stages (128 KiB at D = 128)
   static bool once = false;
   if (!once) {
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true>, smem_a);
     set_smem(attn_bwd_dkdv8_k<D, CAUSAL, true, true>, smem_a);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL>, smem_b);
     set_smem(attn_bwd_dq_ds_k<D, CAUSAL, true>, smem_b);
+    if constexpr (D == 128) set_smem(attn_bwd_dq_ring_k<D, CAUSAL>, smem_r);
     once = true;
   }
   const int64_t LkP = ds_rows(Lk), LqP = ds_cols(Lq);
+  // dS^T layout (ds_layout): row stride and 128-query block stride
+  const bool blk = (g_bwd_stage & 8) != 0;
+  const int64_t ldst = blk ? 128 : LqP, st_blk = blk ? LkP * 128 : 128;
   if (g_bwd_stage & 1)
     attn_bwd_dkdv8_k<D, CAUSAL, true, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, ldst, LkP * LqP, st_blk);
   else
     attn_bwd_dkdv8_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lk, 128) * H * B), 512, smem_a, s>>>(
-        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, LqP, LkP * LqP);
-  if (g_bwd_stage & 2)
+        q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, dk, lddk, dv, lddv, H, Lq, Lk, scale, ks, ds, ldst, LkP * LqP, st_blk);
+  if (D == 128 && (g_bwd_stage & 4))
+    attn_bwd_dq_ring_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_r, s>>>(
+        k, ldk, ds, ldst, LkP * LqP, st_blk, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+  else if (g_bwd_stage & 2)
     attn_bwd_dq_ds_k<D, CAUSAL, true><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
-        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+        k, ldk, ds, ldst, LkP * LqP, st_blk, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   else
     attn_bwd_dq_ds_k<D, CAUSAL><<<(unsigned)(cdiv(Lq, 128) * H * B), 256, smem_b, s>>>(
-        k, ldk, ds, LqP, LkP * LqP, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
+        k, ldk, ds, ldst, LkP * LqP, st_blk, (int)LkP, dq, lddq, H, Lq, Lk, scale, ks);
   return cullavo_check_launch("attn_bwd");
 }
 
@@ -2002,7 +2163,7 @@ extern "C" int cullavo_attn_set_stage(int buffer_loads) {
 
 extern "C" int cullavo_attn_set_bwd_stage(int mode) {
   const int prev = g_bwd_stage;
-  if (mode >= 0 && mode <= 3) g_bwd_stage = mode;
+  if (mode >= 0 && mode <= 15) g_bwd_stage = mode;
   return prev;
 }
 

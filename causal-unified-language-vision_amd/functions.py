@@ -46,6 +46,10 @@ def _lin_act(x, w, b, act, keep_preact):
 # per CU each) slow each other more than the filled tails gain; with the compute stream at high
 # priority 386.2 vs 388.4 (noise level), so the single stream stays the default.
 DW_STREAM = os.environ.get("CULLAVO_DW_STREAM", "off")
+# the down-projection weight gradient on the side stream, launched before the SwiGLU-fused dX GEMM so
+# the two share the CUs (CULLAVO_SWG_OVERLAP=1, A/B): the dX GEMM's epilogue bursts (gate|up read,
+# d(gate|up) write) then meet the dW GEMM's long K-loops instead of each other
+SWG_OVERLAP = os.environ.get("CULLAVO_SWG_OVERLAP", "0") == "1"
 # SwiGLU backward in the down-projection dX GEMM's epilogue (CULLAVO_FUSED_SWIGLU_BWD=0: the
 # separate swiglu_bwd kernel, for A/B)
 FUSED_SWIGLU_BWD = os.environ.get("CULLAVO_FUSED_SWIGLU_BWD", "1") != "0"
@@ -121,9 +125,10 @@ def _join_at_end(st):
         st["queued"] = False
 
 
-def _dw(dy, x, g, beta, *params):
-    """dW GEMM into the arena slot g, then commit(params) (which may launch DP buckets)."""
-    if DW_STREAM == "off" or not dy.is_cuda:
+def _dw(dy, x, g, beta, *params, side=False):
+    """dW GEMM into the arena slot g, then commit(params) (which may launch DP buckets); side: on the
+    side stream whatever DW_STREAM says."""
+    if (DW_STREAM == "off" and not side) or not dy.is_cuda:
         ops.linear_dw(dy, x, g, beta=beta)
         commit(*params)
         return
@@ -140,10 +145,10 @@ def _dw(dy, x, g, beta, *params):
     torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_at_end(st))
 
 
-def _write_dw(dy, x, w):
+def _write_dw(dy, x, w, side=False):
     if trainable(w):
         g, beta = grad_slot(w)
-        _dw(dy, x, g, beta, w)
+        _dw(dy, x, g, beta, w, side=side)
 
 
 def _write_bias(dy, b):
@@ -233,14 +238,19 @@ class LlamaLayerFn(torch.autograd.Function):
         # MLP. Without a LoRA adapter on down_proj the SwiGLU backward runs in the epilogue of
         # the down-projection dX GEMM (dh never stored); with one, dh collects the adapter's
         # share first (bitwise the same arithmetic either way, tests/test_ops_gpu.py).
-        if lg["down"] is NO_LORA and FUSED_SWIGLU_BWD and gu.dtype == torch.bfloat16:
+        fused_swg = lg["down"] is NO_LORA and FUSED_SWIGLU_BWD and gu.dtype == torch.bfloat16
+        overlap = fused_swg and SWG_OVERLAP and dh3.is_cuda
+        if overlap:
+            _write_dw(dh3, a, layer.mlp.down_proj.weight, side=True)
+        if fused_swg:
             dgu = layer.linear_dx(dh3, "down", swiglu_gu=gu)
         else:
             da = layer.linear_dx(dh3, "down")
             lg["down"].backward(dh3, a, u_d, da, tr, seed)
             dgu = ops.swiglu_bwd(da, gu)
             del da
-        _write_dw(dh3, a, layer.mlp.down_proj.weight)
+        if not overlap:
+            _write_dw(dh3, a, layer.mlp.down_proj.weight)
         dx2 = layer.linear_dx(dgu, "gu")
         lg["gu"].backward(dgu, x2, u_gu, dx2, tr, seed)
         if trainable(layer.mlp.gate_proj.weight):

@@ -331,11 +331,14 @@ int cullavo_attn_set_bwd_tiles(int mode);
    Results are identical. Other
    values leave the setting; returns the previous setting. Not thread-safe. */
 int cullavo_attn_set_stage(int buffer_loads);
-/* A/B switch for the backward's tile staging, two bits: bit 0 = the 8-wave dK/dV kernel's
+/* A/B switch for the backward's tile staging, three bits: bit 0 = the 8-wave dK/dV kernel's
    (modes 4, 5, 7) Q / dO tiles, bit 1 = the mode-7 dQ kernel's K / dS^T tiles by LDS-DMA
    straight into the swizzled image (else through registers and ds_write); the default is 1
    (round 5: with LDS-DMA staging the dK/dV kernel's fragment reads are inline asm, one step ahead
-   of the MFMAs). Results are identical. Other values leave the setting; returns the previous one. */
+   of the MFMAs). Bit 2 (round 6, head dim 128): the mode-7 dQ kernel as a 4-stage LDS-DMA ring,
+   one workgroup per CU with three 64-key tiles in flight (takes precedence over bit 1). Bit 3
+   (round 6): the dS^T workspace blocked by 128-query column blocks (a dQ tile is one contiguous
+   16 KiB run instead of 64 rows of 256 B). Results are identical. Other values leave the setting; returns the previous one. */
 int cullavo_attn_set_bwd_stage(int mode);
 /* Attention forward's deferred rescale (guide T13): the running row max and the O / l rescale
    move only on K/V tiles where some row's max grew by more than `threshold` (log2 units, in

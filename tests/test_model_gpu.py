@@ -261,8 +261,9 @@ def test_dw_side_stream_bitwise(monkeypatch):
     ids, mask, pix, labels = inputs()
     ids2, mask2, pix2, labels2 = inputs(seed=5)
     res = {}
-    for mode in ("off", "side"):
-        monkeypatch.setattr(FN, "DW_STREAM", mode)
+    for mode in ("off", "side", "swg"):  # swg: only the down-projection dW, beside the SwiGLU dX GEMM
+        monkeypatch.setattr(FN, "DW_STREAM", "off" if mode == "swg" else mode)
+        monkeypatch.setattr(FN, "SWG_OVERLAP", mode == "swg")
         m = build()
         opt = FusedAdamW(list(m.arenas.values()), lr=1e-3)
         seen = []
@@ -275,8 +276,9 @@ def test_dw_side_stream_bitwise(monkeypatch):
             opt.step()
         seen.append(torch.cat([ar.flat.clone() for ar in m.arenas.values()]))
         res[mode] = seen
-    for i, (a, b) in enumerate(zip(res["off"], res["side"])):
-        assert torch.equal(a, b), i
+    for other in ("side", "swg"):
+        for i, (a, b) in enumerate(zip(res["off"], res[other])):
+            assert torch.equal(a, b), (other, i)
 
 
 def test_adamw_overlap_bitwise():

@@ -135,7 +135,7 @@ def test_attention_rows_past_end_next_to_nan(B, H, L, D, causal):
         base = None
         for tiles in ((7, 4) if D == 128 else (0, 4)):
             Lb.cullavo_attn_set_bwd_tiles(tiles)
-            for st in (0, 1, 2, 3):
+            for st in range(16):  # bit 2: the LDS-DMA ring dQ kernel (D = 128), bit 3: blocked dS^T
                 Lb.cullavo_attn_set_bwd_stage(st)
                 dq, dk, dv = ops.attn_bwd(qd, kd, vd, od, dod, lse_d, **kw)
                 torch.cuda.synchronize()

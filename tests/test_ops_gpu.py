@@ -747,10 +747,11 @@ def test_attention_bwd_tile_modes_bitwise(D, causal):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16)), f"d{name} mode 7 vs 4"
     # the LDS-DMA staging (cullavo_attn_set_bwd_stage) stages the same bytes (rows past the end as
     # zeros): modes 4 and 7 bitwise equal to the register staging, for the dK/dV kernel's Q / dO
-    # (bit 0) and the dQ-from-dS kernel's K / dS^T (bit 1)
+    # (bit 0), the dQ-from-dS kernel's K / dS^T (bit 1), its LDS-DMA ring form (bit 2, D = 128) and
+    # the blocked dS^T layout (bit 3)
     prev_st = _lib.lib().cullavo_attn_set_bwd_stage(1)
     try:
-        for st in (1, 2, 3):
+        for st in range(1, 16):
             _lib.lib().cullavo_attn_set_bwd_stage(st)
             for mode8 in (4, 7):
                 _lib.lib().cullavo_attn_set_bwd_tiles(mode8)

@@ -9,7 +9,9 @@ FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
 MFMA busy fraction = (SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs),
 summed over the dispatches (time-weighted).
 
-  python tools/pmc_family.py <fetch.csv> <write.csv> <sq.csv> "<kernel name>" <workload key> > record.json
+  python tools/pmc_family.py <fetch.csv> <write.csv> <sq.csv> "<kernel name>[||<kernel name>...]" <workload key> > records.json
+
+(one record per kernel name; several names give a JSON list)
 
 The record (keyed by workload and kernel) goes into profiles/roofline_traffic.json's "records",
 which bench.py reads for the same (workload, kernel) pair only.
@@ -24,6 +26,7 @@ from collections import defaultdict
 def name_pattern(kname):
     """kname as a regex: "<MODE>" matches every epilogue-mode instantiation of a kernel, "*" one
     integer template argument (bench.gemm_kernel_name's EPI wildcard)"""
+    kname = kname.split(" M-split")[0]  # bench's family suffix: the head rows' kernel is the one profiled
     pat = re.escape(kname).replace(re.escape("<MODE>"), r"<\d+>").replace(re.escape("*"), r"\d+")
     return re.compile(pat)
 
@@ -41,8 +44,13 @@ def per_dispatch(path, kname):
 
 
 def main():
-    fcsv, wcsv, scsv, kname = sys.argv[1:5]
+    fcsv, wcsv, scsv, knames = sys.argv[1:5]
     workload = sys.argv[5] if len(sys.argv) > 5 else "config3-full"
+    recs = [record(fcsv, wcsv, scsv, k, workload) for k in dict.fromkeys(knames.split("||"))]
+    print(json.dumps(recs[0] if len(recs) == 1 else recs, indent=1))
+
+
+def record(fcsv, wcsv, scsv, kname, workload):
     f, w, q = per_dispatch(fcsv, kname), per_dispatch(wcsv, kname), per_dispatch(scsv, kname)
     fetch = [v["FETCH_SIZE"] for v in f.values() if "FETCH_SIZE" in v]
     write = [v["WRITE_SIZE"] for v in w.values() if "WRITE_SIZE" in v]
@@ -60,7 +68,7 @@ def main():
         if wave:
             out["sq_wait_any_frac"] = round(sum(v.get("SQ_WAIT_ANY", 0.0) for v in q.values()) / wave, 4)
             out["sq_wait_inst_any_frac"] = round(sum(v.get("SQ_WAIT_INST_ANY", 0.0) for v in q.values()) / wave, 4)
-    print(json.dumps(out, indent=1))
+    return out
 
 
 if __name__ == "__main__":

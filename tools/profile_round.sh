@@ -19,5 +19,7 @@ for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "SQ_VALU_MFMA_BUSY_CYCLES GRBM
   CNT=${pass%%:*}; TAG=${pass##*:}
   timeout -s KILL 300 rocprofv3 --pmc $CNT --kernel-include-regex gemm -d $OUT/pmc_$TAG -o p --output-format csv -- python bench.py --steps 1 --warmup 1 $ARGS > $OUT/pmc_$TAG.log 2>&1
 done
-python tools/pmc_family.py $OUT/pmc_fetch/p_counter_collection.csv $OUT/pmc_write/p_counter_collection.csv $OUT/pmc_sq/p_counter_collection.csv "$KERNEL" "$WL" > $OUT/roofline_traffic.json
+# records for the given kernel and for the roofline kernel the traced bench line itself names
+RK=$(python -c "import json; l=[x for x in open('$OUT/bench_traced.log') if x.startswith('{')]; print(json.loads(l[-1])['roofline']['kernel'].split(':')[0])")
+python tools/pmc_family.py $OUT/pmc_fetch/p_counter_collection.csv $OUT/pmc_write/p_counter_collection.csv $OUT/pmc_sq/p_counter_collection.csv "$KERNEL||$RK" "$WL" > $OUT/roofline_traffic.json
 echo done
