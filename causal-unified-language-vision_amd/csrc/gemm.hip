@@ -740,8 +740,11 @@ double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 // + 64: fc1 at 256x256 is 2,320 tiles = 9.06 rounds -> 10; fc2 / o at 288x256 are 516 tiles =
 // 2.02 rounds -> 3). The plan then runs rows [0, m_main) (m_main = a multiple of the tile height)
 // on that tile and the remaining rows as a second, thin product (128x128 tiles, split over K
-// when the caller gives the workspace), if that is estimated at least 5 % faster.
-int g_msplit = 1;
+// when the caller gives the workspace), if that is estimated faster: g_msplit 2 (the default since
+// round 6) on any estimated gain, 1 only on >= 5 % (round 5's rule, which left fc1 unsplit: its
+// estimate is 3 %; split, fc1 runs 902 -> 928 TF/s and the ViT step 2505 -> 2518 img/s,
+// profiles/r06/gemm/msplit_eager_ab.txt).
+int g_msplit = 2;
 // 288-row tiles at K < 2048 (cullavo_gemm_set_epilogue bit 9, A/B; off: the round-3 exclusion below)
 int g_short288 = 0;
 // the thin product's time: its split-K launch + reduce cost 16-19 us at the ViT shapes (64 rows:
@@ -810,7 +813,7 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_
       }
     }
   }
-  if (m_main && best_split < 0.95 * best) {
+  if (m_main && best_split < (g_msplit == 2 ? 0.999 : 0.95) * best) {
     *m_main = mm_split;
     return bid_split;
   }
@@ -1145,6 +1148,6 @@ extern "C" int cullavo_gemm_ex(const cullavo_gemm_desc* desc, void* stream) {
 // A/B switch for the M-tail split of the automatic plan (1 = on, the default); returns the previous
 extern "C" int cullavo_gemm_set_msplit(int on) {
   const int prev = g_msplit;
-  g_msplit = on ? 1 : 0;
+  g_msplit = on == 2 ? 2 : on ? 1 : 0;
   return prev;
 }

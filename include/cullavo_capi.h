@@ -167,7 +167,8 @@ int cullavo_gemm_set_tile_rate(int mode, float tflops, float* previous);
 /* M-tail split of the automatic plan (tuning/A-B switch, 1 = on, the default): when M is just past
    a multiple of the chosen tile height, the head rows run on that tile in whole rounds and the
    remaining rows as a second, thin product (split over K when cullavo_gemm_workspace sized the
-   caller's workspace for it). Returns the previous setting. */
+   caller's workspace for it). 2 (the default since round 6) = split wherever the plan's model
+   estimates a gain; 1 = only where it estimates >= 5 % (round 5). Returns the previous setting. */
 int cullavo_gemm_set_msplit(int on);
 /* Tile order of the 8-wave kernels (tuning/A-B switch): > 0 = groups of that many M-tiles
    sweep the N-tiles, < 0 = groups of -group N-tiles sweep the M-tiles (default -4); each XCD

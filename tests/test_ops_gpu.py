@@ -94,7 +94,7 @@ def test_gemm_epilogues(act, tile_mode, epi_mode):
 
 
 @pytest.mark.parametrize("M,N,K,act", [(36928, 1024, 4096, "none"), (18496, 2048, 4096, "quick_gelu"),
-                                         (18496, 1024, 4096, "none")])
+                                         (18496, 1024, 4096, "none"), (36928, 4096, 1024, "quick_gelu")])
 def test_gemm_msplit(M, N, K, act):
     """M-tail split (cullavo_gemm_set_msplit; the ViT's M = 64 x 577 = 36928): the head rows run in
     whole rounds of the planned tile and the rest as a thin split-K product. Head rows are

@@ -3,6 +3,8 @@ shapes, interleaved rounds in one process (guide §5.4 rule 24), random bf16 ope
   direct : the default (direct register epilogue, persistent 256 / 288-row forward kernels)
   lds    : bit 7 (the LDS-staged epilogue and the round-5 persistent kernel)
   nopers : bit 5 (no persistent forward kernel; direct epilogue in the data-parallel kernels)
+  eager    : cullavo_gemm_set_msplit(2) (the M-tail split wherever the plan estimates a gain; the default
+             since round 6), msplit5: set_msplit(1) (only >= 5 %, round 5)
   short288 : bit 9 (288-row tiles allowed at K < 2048), short288p: bits 9+8 (and the persistent 288)
 Each case runs with the epilogue it has in the step (plain, residual, bias, quick_gelu).
 
@@ -29,7 +31,8 @@ CASES = [  # name, M, N, K, a_layout, b_layout, epilogue
     ("vit_fc1", 36928, 4096, 1024, 0, 0, "qgelu"), ("vit_qkv", 36928, 3072, 1024, 0, 0, "bias"),
     ("vit_o", 36928, 1024, 1024, 0, 0, "bias_res"), ("vit_fc2", 36928, 1024, 4096, 0, 0, "bias_res"),
 ]
-ALL_MODES = {"direct": 1, "lds": 1 | 128, "nopers": 1 | 32, "short288": 1 | 512, "short288p": 1 | 512 | 256}
+MSPLIT = {"eager": 2, "msplit5": 1}  # modes that set cullavo_gemm_set_msplit (default 2) besides the epilogue bits
+ALL_MODES = {"eager": 1, "msplit5": 1, "direct": 1, "lds": 1 | 128, "nopers": 1 | 32, "short288": 1 | 512, "short288p": 1 | 512 | 256}
 
 
 def main():
@@ -62,6 +65,7 @@ def main():
         for r in range(a.rounds):
             for m, bits in MODES.items():
                 L.cullavo_gemm_set_epilogue(bits)
+                L.cullavo_gemm_set_msplit(MSPLIT.get(m, 2))
                 run()
                 if r == 0:
                     torch.cuda.synchronize()
@@ -78,8 +82,10 @@ def main():
         line = f"{name:11s} {M}x{N}x{K} ({al},{bl}) {epi:8s}"
         for m, bits in MODES.items():
             L.cullavo_gemm_set_epilogue(bits)
+            L.cullavo_gemm_set_msplit(MSPLIT.get(m, 2))
             line += f" | {m} [{L.cullavo_gemm_plan(M, N, K, al, bl, None)}] {statistics.median(res_t[m]):7.1f}"
         L.cullavo_gemm_set_epilogue(base)
+        L.cullavo_gemm_set_msplit(2)
         print(line + f" | bitwise {'equal' if same else 'DIFFERENT'}", flush=True)
         del A, B, C, bias, res
 
