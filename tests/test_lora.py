@@ -304,9 +304,12 @@ def test_lora_fused_msplit_short_tail(T):
     from cullavo_amd import _lib, ops
     inn, out, r, n = 4096, 4096, 64, 1
     L = _lib.lib()
-    plan = L.cullavo_gemm_plan(T, n * out, inn, 0, 0, ctypes.byref(ctypes.c_int64(0)))
-    if T % 288 <= 16:
-        assert plan < 100, plan  # no split with a <= 16-row tail
+    grid = ctypes.c_int64(0)
+    plan = L.cullavo_gemm_plan(T, n * out, inn, 0, 0, ctypes.byref(grid))
+    if plan >= 100:  # a split leaves more than 16 rows to the tail (the head: whole M-tiles of the plan's tile)
+        bm = {2: 256, 3: 192, 10: 288}[plan - 100]
+        head = grid.value // -(-(n * out) // 256) * bm
+        assert T - head > 16, (plan, head)
     ar, grp, s, names = _lora_arena(n, out, inn, r, 70)
     x = rnd((T, inn), 71).cuda()
     W = rnd((n * out, inn), 72, inn ** -0.5).cuda()
