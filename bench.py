@@ -535,7 +535,7 @@ def gemm_kernel_name(M, N, K, al=0, bl=0, lora=False):
         # the persistent forward kernels (gemm.hip launch256p / launch288pd), one instantiation per
         # epilogue mode (0 plain, 1 bias/residual, 2 activation); one block per CU
         if t in (2, 10) and (al, bl) == (0, 0) and not lora and ep & 1 and not ep & 32 and (
-                t == 2 or (direct and ep & 256)):
+                t == 2 or (direct and (ep & 256 or K < 2048 or N <= 2048))):
             return f"gemm256pd_k<*, {256 if t == 2 else 288}>" if direct else "gemm256p_k<MODE>"
         return None
     if tile >= 100:  # the M-tail split: the head rows' kernel (+ a thin split-K product for the rest)

@@ -572,12 +572,15 @@ int lean_mode(const GemmArgs& p) {
 // C addressable by one buffer descriptor (the direct epilogue's stores)
 bool c_fits_rsrc(const GemmArgs& p) { return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB; }
 
-// the persistent 288-row direct kernel for a lean (0,0) product (the 7B forward products the plan puts
-// on 288-row tiles); -1: not eligible. Opt-in (cullavo_gemm_set_epilogue bit 8): on one box
+// the persistent 288-row direct kernel for a lean (0,0) product; -1: not eligible. Always at K < 2048
+// or N <= 2048 (the ViT's products: K = 1024 on 288-row tiles since round 6, fc2 N = 1024): fc1 / o
+// 920 / 825 -> 940 / 880 TF/s with the plan's 288-row M-split; ViT step 2481 (round 5's plan) ->
+// 2488 (288 rows at short K) -> 2496 img/s (and fc2 persistent), alternating on one box
+// (profiles/r06/gemm/vit288_ab.txt). Otherwise opt-in (cullavo_gemm_set_epilogue bit 8): on one box
 // (tools/epi_ab.py, profiles/r06/gemm/epi_ab.txt) it beat the data-parallel 288-row direct kernel on
 // gate|up (1349 vs 1340 TF/s) but lost on q|k|v, o and down (1358 / 1284 / 1305 vs 1390 / 1317 / 1314)
 int launch288pd(const GemmArgs& p, hipStream_t s) {
-  if (!(p.epi_lds & 256)) return -1;
+  if (!(p.epi_lds & 256) && p.K >= 2048 && p.N > 2048) return -1;
   if (p.part != nullptr || !p.epi_lds || (p.epi_lds & (128 | 32)) || !p.dma_pre || !c_fits_rsrc(p)) return -1;
   const int mode = lean_mode(p);
   if (mode == 0) return launch256pd_m<0, 288>(p, s);
@@ -745,8 +748,9 @@ double g_tile_rate[3] = {1300.0, 1150.0, 1360.0};
 // estimate is 3 %; split, fc1 runs 902 -> 928 TF/s and the ViT step 2505 -> 2518 img/s,
 // profiles/r06/gemm/msplit_eager_ab.txt).
 int g_msplit = 2;
-// 288-row tiles at K < 2048 (cullavo_gemm_set_epilogue bit 9, A/B; off: the round-3 exclusion below)
-int g_short288 = 0;
+// 288-row tiles at K < 2048 (round 6, with the persistent 288-row direct kernel: launch288pd);
+// cullavo_gemm_set_epilogue bit 9 restores the round-3 exclusion below
+int g_short288 = 1;
 // the thin product's time: its split-K launch + reduce cost 16-19 us at the ViT shapes (64 rows:
 // profiles/r05/vit/vit_kernel_trace.txt), so a split pays only where it saves more than that --
 // fc2 (K = 4096: 3 -> 2 rounds of 288-row tiles), not fc1 / o (K = 1024)
@@ -783,9 +787,10 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int a_layout, int force, int64_
   int64_t mm_split = 0;
   for (const C& c : cands) {
     if ((c.id == kT192x256 || c.id == kT288x256) && a_layout != 0) continue;
-    // 288 rows only for long K: with 16 K-tiles (the ViT's K = 1024 products) its larger
-    // per-tile prologue and 144 KiB epilogue cost more than the rounds it saves (config 2:
-    // fc1 36928x4096x1024 at 815 TF/s against 865 for the 256-row tile)
+    // round 3: 288 rows only for long K -- with 16 K-tiles (the ViT's K = 1024 products) its larger
+    // per-tile prologue and 144 KiB LDS-staged epilogue cost more than the rounds it saved (config 2:
+    // fc1 36928x4096x1024 at 815 TF/s against 865 for the 256-row tile); with the direct epilogue
+    // and the persistent 288-row kernel (round 6) short K takes it too, unless bit 9
     if (c.id == kT288x256 && K < 2048 && !g_short288) continue;
     if (c.rate <= 0.0) continue;
     const double t = seconds(c, M);
@@ -870,13 +875,13 @@ extern "C" int cullavo_gemm_set_dma(int precomputed) {
 
 // A/B switch for the LDS-staged epilogue of the 8-wave kernels (1 = on, the default)
 extern "C" int cullavo_gemm_set_epilogue(int lds_staged) {
-  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 508) | (g_short288 << 9);
+  const int prev = (g_epi_lds & 1) | (g_nt_store << 1) | (g_epi_lds & 508) | (g_short288 ? 0 : 512);
   g_epi_lds = lds_staged & 509;  // bit 0 LDS-staged; bits 2 / 3 / 4 disable its bias-residual / plain /
                                  // activation + SwiGLU-backward paths; bit 5 the persistent forward kernel;
                                  // bit 6 the prefetching SwiGLU-backward instantiation; bit 7 the direct
                                  // (register) epilogue of the lean cases; bit 8 the persistent 288-row
                                  // direct forward kernel (opt-in)
-  g_short288 = (lds_staged >> 9) & 1;  // bit 9: 288-row tiles at K < 2048 (A/B)
+  g_short288 = !((lds_staged >> 9) & 1);  // bit 9: no 288-row tiles at K < 2048 (round 5's plan)
   g_nt_store = (lds_staged >> 1) & 1;
   return prev;
 }

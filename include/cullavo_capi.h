@@ -186,8 +186,9 @@ int cullavo_gemm_set_splitk_target(int blocks);
    (same values): bit 6 keeps the SwiGLU-backward dX on the general epilogue path instead of its
    prefetching instantiation; bit 7 keeps the LDS-staged epilogue for the lean cases instead of
    the direct (register, 16-B buffer store) epilogue and its persistent forward kernel; bit 8 opts
-   into the persistent 288-row direct forward kernel; bit 9 lets the plan take 288-row tiles at
-   K < 2048 (A/B).
+   into the persistent 288-row direct forward kernel at K >= 2048 and N > 2048 (elsewhere it is the
+   default);
+   bit 9 keeps the plan off 288-row tiles at K < 2048 (round 5's plan; the default takes them).
    Returns the previous setting. */
 int cullavo_gemm_set_epilogue(int lds_staged);
 /* Tuning/A-B switch for the 8-wave 256-row kernels: 1 = per-lane LDS-DMA source offsets

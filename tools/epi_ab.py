@@ -5,7 +5,9 @@ shapes, interleaved rounds in one process (guide §5.4 rule 24), random bf16 ope
   nopers : bit 5 (no persistent forward kernel; direct epilogue in the data-parallel kernels)
   eager    : cullavo_gemm_set_msplit(2) (the M-tail split wherever the plan estimates a gain; the default
              since round 6), msplit5: set_msplit(1) (only >= 5 %, round 5)
-  short288 : bit 9 (288-row tiles allowed at K < 2048), short288p: bits 9+8 (and the persistent 288)
+  no288    : bit 9 (no 288-row tiles at K < 2048: round 5's plan; since round 6 the default takes them,
+             on the persistent 288-row kernel). short288 / short288p (bits 9 / 9 + 8) were the round-6
+             A/B names while bit 9 meant "allow"; with the flipped bit they now mean no288 / no288 + bit 8
 Each case runs with the epilogue it has in the step (plain, residual, bias, quick_gelu).
 
   python tools/epi_ab.py [--rounds 5]
@@ -32,7 +34,7 @@ CASES = [  # name, M, N, K, a_layout, b_layout, epilogue
     ("vit_o", 36928, 1024, 1024, 0, 0, "bias_res"), ("vit_fc2", 36928, 1024, 4096, 0, 0, "bias_res"),
 ]
 MSPLIT = {"eager": 2, "msplit5": 1}  # modes that set cullavo_gemm_set_msplit (default 2) besides the epilogue bits
-ALL_MODES = {"eager": 1, "msplit5": 1, "direct": 1, "lds": 1 | 128, "nopers": 1 | 32, "short288": 1 | 512, "short288p": 1 | 512 | 256}
+ALL_MODES = {"no288": 1 | 512, "eager": 1, "msplit5": 1, "direct": 1, "lds": 1 | 128, "nopers": 1 | 32, "short288": 1 | 512, "short288p": 1 | 512 | 256}
 
 
 def main():
