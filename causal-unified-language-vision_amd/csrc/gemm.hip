@@ -569,8 +569,11 @@ int lean_mode(const GemmArgs& p) {
   return -1;
 }
 
-// C addressable by one buffer descriptor (the direct epilogue's stores)
-bool c_fits_rsrc(const GemmArgs& p) { return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB; }
+// C (the direct epilogue's stores) and the residual (its loads) addressable by one buffer descriptor each
+bool c_fits_rsrc(const GemmArgs& p) {
+  return ((p.M - 1) * p.ldc + p.N) * 2 < (int64_t)kOOB &&
+         (p.residual == nullptr || ((p.M - 1) * p.ldr + p.N) * 2 < (int64_t)kOOB);
+}
 
 // the persistent 288-row direct kernel for a lean (0,0) product; -1: not eligible. Always at K < 2048
 // or N <= 2048 (the ViT's products: K = 1024 on 288-row tiles since round 6, fc2 N = 1024): fc1 / o

@@ -659,16 +659,34 @@ DEV void direct_epilogue(const GemmArgs& p, const f32x4 (&acc)[TMW][4], __amdgpu
   const bool res = MODE == 1 && p.residual != nullptr;
   // this lane's chunk column (after the swap) for pair pr: wn0 + (2 pr + (g & 1)) * 16 + (g >> 1) * 8
   const int64_t nc0 = wn0 + (g & 1) * 16 + (g >> 1) * 8;
+  // every residual chunk of the wave loaded before the first store (vmcnt retires in issue order,
+  // so a load issued after a store would wait for that store too: per 16-row group, a store-drain
+  // latency); buffer loads on the residual's own descriptor (out-of-range chunks read as zeros and
+  // are not stored), one 32-bit offset each
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.residual, (short)0, res ? (int)(((p.M - 1) * p.ldr + p.N) * 2) : 0, 0x00020000);
+  auto res_load = [&](int tm, u16x8 (&r)[2]) {
+    const int64_t m = wm0 + tm * 16 + (lane & 15);
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int64_t n = nc0 + pr * 32;
+      const unsigned off = (m < p.M && n < p.N) ? (unsigned)((m * p.ldr + n) * 2) : 0x80000000u;
+      r[pr] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+    }
+  };
+  u16x8 rall[TMW][2];
+  if (res) {
+#pragma unroll
+    for (int tm = 0; tm < TMW; ++tm) res_load(tm, rall[tm]);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every residual load issued before the first store
 #pragma unroll
   for (int tm = 0; tm < TMW; ++tm) {
     const int64_t m = wm0 + tm * 16 + (lane & 15);
     u16x8 rv[2];
     if (res) {  // this tm's two residual chunks (same rows / columns as the stores below)
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const int64_t n = nc0 + pr * 32;
-        if (m < p.M && n < p.N) rv[pr] = *reinterpret_cast<const u16x8*>(p.residual + m * p.ldr + n);
-      }
+      rv[0] = rall[tm][0];
+      rv[1] = rall[tm][1];
     }
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
