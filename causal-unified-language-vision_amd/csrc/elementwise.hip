@@ -7,6 +7,9 @@ namespace {
 
 DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 DEV float siluf_(float x) { return x / (1.f + __expf(-x)); }
+// swiglu_bwd_k's sigmoid: the expression of gemm_common.h sigmoid_rcp (the SwiGLU backward fused into
+// the down-projection dX GEMM's epilogue), so the two paths are bitwise equal
+DEV float sigmoid_rcp_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // one 16-B vector per thread (the loops stay grid-stride): against a 2048-block cap the SwiGLU
 // kernels run 10 % faster (tools/stream_bench.py: 5.1 -> 5.7 TB/s), more loads in flight per CU
@@ -41,7 +44,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ d, con
     load8(gu + r * 2 * F + F + c, uv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float s = sigmoidf_(gv[j]);
+      const float s = sigmoid_rcp_(gv[j]);
       const float silu = gv[j] * s;
       b[j] = dv[j] * Elt<T>::rnd(silu);
       a[j] = dv[j] * uv[j] * s * (1.f + gv[j] * (1.f - s));

@@ -202,7 +202,10 @@ DEV int xcd_remap(int bid, int nwg) {
 // of the SwiGLU, rounded to bf16 as the unfused path stores it; with g = gu[m][n], u = gu[m][F + n]
 // (gu = p.residual, F = p.N) it writes dg to C[m][n] and du to C[m][F + n], in the arithmetic of
 // swiglu_bwd_k (elementwise.hip) so the fused and unfused paths are bitwise equal.
-DEV float sigmoid_ieee(float x) { return 1.f / (1.f + __expf(-x)); }
+// the SwiGLU backward's sigmoid: v_rcp_f32 (1 ulp) instead of the IEEE division sequence (~10 VALU
+// ops; the SwiGLU-backward dX 1001-1016 -> 1013-1032 TF/s, profiles/r06/gemm/swiglu_rcp_ab.txt);
+// elementwise.hip swiglu_bwd_k uses the same expression, so the fused and unfused paths stay bitwise
+DEV float sigmoid_rcp(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // the arithmetic of one lane's NV columns: dg -> oa, du -> ob (shared by every SwiGLU-backward path)
 template <int NV, typename UV>
@@ -211,7 +214,7 @@ DEV void swiglu_bwd_math(const float* acc, float alpha, const UV& gv, const UV& 
   for (int j = 0; j < NV; ++j) {
     const float dv = round_bf(acc[j] * alpha);
     const float g = bf2f(gv[j]), u = bf2f(uv[j]);
-    const float sg = sigmoid_ieee(g);
+    const float sg = sigmoid_rcp(g);
     const float silu = g * sg;
     ob[j] = f2bf(dv * round_bf(silu));
     oa[j] = f2bf(dv * u * sg * (1.f + g * (1.f - sg)));

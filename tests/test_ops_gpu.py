@@ -427,6 +427,16 @@ def test_swiglu_bwd_fused_in_dx_gemm(M, Fd, d, tile):
         _lib.lib().cullavo_gemm_set_tile(prev)
     assert torch.equal(fused, ref)
     assert torch.equal(fused_t, ref)
+    # the prefetching LDS-staged form (default) against the rolled general path (bit 6)
+    L = _lib.lib()
+    prev_t, prev_e = L.cullavo_gemm_set_tile(tile), L.cullavo_gemm_set_epilogue(1)
+    try:
+        for bits in (1 | 64,):
+            L.cullavo_gemm_set_epilogue(bits)
+            assert torch.equal(ops().linear_dx(dy, w, swiglu_gu=gu), ref), bits
+    finally:
+        L.cullavo_gemm_set_tile(prev_t)
+        L.cullavo_gemm_set_epilogue(prev_e)
     with pytest.raises(Exception):
         ops().linear_dx(dy, w, swiglu_gu=gu[:, :Fd])
 
