@@ -1035,9 +1035,10 @@ static int gemm_impl(const cullavo_gemm_desc& d, void* stream, int tile_hint) {
     p.lora_b = (const u16*)d.lora_b;
     p.lora_out = d.lora_out;
     p.lora_scale = d.lora_scale;
-    // the 288-row tile where the plan takes it (the N = 4096 products: 2 rounds instead of 3)
-    // (the direct epilogue is not used here: beside the fused LoRA's registers it spills ~100 VGPRs)
-    if (choose_tile(M, N, K, 0, g_force_tile) == kT288x256)
+    // the 288-row tile where the plan takes it (the N = 4096 products: 2 rounds instead of 3), at
+    // K >= 2048 only: the direct epilogue is not used here (beside the fused LoRA's registers it spills
+    // ~100 VGPRs), and with the LDS-staged one short-K 288-row tiles lose (round 3; choose_tile)
+    if (choose_tile(M, N, K, 0, g_force_tile) == kT288x256 && (K >= 2048 || g_force_tile == kT288x256))
       return launch256<0, 0, CULLAVO_DT_BF16, 288, 256, true>(p, s);
     return launch256<0, 0, CULLAVO_DT_BF16, 256, 256, true>(p, s);
   }
