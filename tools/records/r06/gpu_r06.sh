@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU pass: targeted tests of the changed kernels first, A/B benches, then the full suite and the
-# default bench line.  bash tools/gpu_r06.sh <tag> [full]
+# default bench line.  bash tools/records/r06/gpu_r06.sh <tag> [full]
 set -o pipefail
 TAG=${1:-r06}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \

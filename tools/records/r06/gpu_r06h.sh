@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 attention backward staging profile: for each bwd stage (cullavo_attn_set_bwd_stage) a kernel
 # trace of tools/attn_bench.py plus one FETCH_SIZE and one SQ pass over the dQ / dK-dV kernels
-#   bash tools/gpu_r06h.sh <tag> [stages...]   (default: 1 5 9 13; optional TESTS=1 first runs the staging tests)
+#   bash tools/records/r06/gpu_r06h.sh <tag> [stages...]   (default: 1 5 9 13; optional TESTS=1 first runs the staging tests)
 set -o pipefail
 TAG=${1:-r06h}; shift || true
 STAGES=${*:-1 5 9 13}
